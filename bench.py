@@ -1,0 +1,303 @@
+"""Benchmark: device-resident AES-256-CBC + HMAC-SHA256 token throughput.
+
+BASELINE.json metric: "device-resident packets/s + GiB/s AES-256-CBC+HMAC-SHA256
+at 1/2/4/8 MI355X".  Workload (BASELINE.json configs[1]):
+2^20 packets x 500 B plaintext per GPU, one link key; one STEP = encrypt+MAC
+of the batch (Token.encrypt, Token.py:87-97) followed by verify+decrypt of the
+tokens it produced (Token.decrypt, Token.py:100-114).  Inputs are generated on
+the device before timing (synthetic, uniform random bytes).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+Multi-GPU: packets are independent, so each rank owns its own 2^20-packet
+shard (weak scaling) and no collective touches the data path; RCCL is used
+only for the barrier and the max-over-ranks reduction of the timings.
+Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# --- roofline model ---------------------------
+# Canonical VALU lane-ops per packet (SURVEY §8(d) constants):
+#   AES block 352, SHA-256 compression 1464, tag compare 8 (decrypt only).
+AES_BLOCK_OPS, SHA_CMP_OPS, TAG_CMP_OPS = 352, 1464, 8
+LDS_LOOKUPS_PER_BLOCK = 224        # 16 per round x 14 rounds (AES-256)
+
+
+def blocks(L):
+    return L // 16 + 1
+
+
+def sha_compressions(L):
+    # ipad/opad midstates are per key; inner hash over iv||ct after the ipad
+    # block, plus one outer compression.
+    return math.ceil((64 + 16 + 16 * blocks(L) + 9) / 64) - 1 + 1
+
+
+def ops_enc(L):
+    return AES_BLOCK_OPS * blocks(L) + SHA_CMP_OPS * sha_compressions(L)
+
+
+def ops_dec(L):
+    return ops_enc(L) + TAG_CMP_OPS
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
+    ap.add_argument("--length", type=int, default=500, help="plaintext bytes per packet")
+    ap.add_argument("--keys", type=int, default=1, help="1 = single link key (c2); 65536 = c3")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 disables)")
+    ap.add_argument("--cpu-workers", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--e2e", action="store_true", default=True, help="also time the PCIe-inclusive path")
+    ap.add_argument("--no-e2e", dest="e2e", action="store_false")
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds, workers, L):
+    """The pure-Python restatement (oracle/cpuref.py, reference work shape)
+    on the host cores, enc+dec round trips of 500 B packets."""
+    if seconds <= 0:
+        return None
+    import multiprocessing as mp
+    from oracle import cpuref  # noqa: F401  (checked importable before forking)
+    if workers <= 0:
+        workers = max(1, min(16, os.cpu_count() or 1))
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(workers) as pool:
+        t0 = time.perf_counter()
+        res = pool.map(_cpu_worker, [(seconds, L, i) for i in range(workers)])
+        wall = time.perf_counter() - t0
+    pkts = sum(r[0] for r in res)
+    busy = max(r[1] for r in res)
+    rate = pkts / busy
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": rate, "unit": "packets/s", "gib_s": rate * L / 2**30, "cores": workers, "kind": "port",
+        "sample": f"{pkts} round trips (encrypt+decrypt) of {L} B packets, one key, oracle/cpuref.py "
+                  f"(pure Python, per-call key schedule like AES.py:83,100) on {workers} processes for "
+                  f"~{seconds:.0f} s each; wall {wall:.1f} s; cpu '{model}'; cpuref/reference speed "
+                  f"ratio measured in the build container: enc 1.64, dec 1.95 (tools/calibrate_cpuref.py)",
+    }
+
+
+def _cpu_worker(arg):
+    seconds, L, seed = arg
+    import random
+    from oracle import cpuref
+    rnd = random.Random(seed)
+    key = bytes(rnd.getrandbits(8) for _ in range(64))
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        pt = bytes(rnd.getrandbits(8) for _ in range(L))
+        iv = bytes(rnd.getrandbits(8) for _ in range(16))
+        tok = cpuref.encrypt(key, iv, pt)
+        st, back = cpuref.decrypt(key, tok)
+        assert st == 0 and back == pt
+        n += 1
+    return n, time.perf_counter() - t0
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import reticulum_amd as rt
+    from reticulum_amd import _native, device
+
+    n, L = args.packets, args.length
+    tl = rt.token_len(L)
+    dev = torch.device("cuda", local)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    pt = torch.randint(0, 256, (n, L), dtype=torch.uint8, device=dev, generator=g)
+    iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
+    tok = torch.empty((n, tl), dtype=torch.uint8, device=dev)
+    back = torch.empty((n, tl - 48), dtype=torch.uint8, device=dev)
+    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    kg = torch.Generator().manual_seed(7)
+    keys = torch.randint(0, 256, (args.keys, 64), dtype=torch.uint8, generator=kg).numpy()
+    ks = rt.KeySet(keys, device=local)
+    key_idx = None
+    if args.keys > 1:
+        key_idx = torch.randint(0, args.keys, (n,), dtype=torch.int32, device=dev, generator=g)
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        device.encrypt_uniform(ks, pt, L, iv, tok, key_idx=key_idx, stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        device.decrypt_uniform(ks, tok, tl, back, out_len, status, key_idx=key_idx, stream=stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness gate on the benchmarked data (size-independent properties)
+    ok = bool((status == 0).all()) and bool((out_len == L).all()) and torch.equal(back[:, :L], pt)
+    if not ok:
+        raise SystemExit("bench: round trip failed on the benchmark batch")
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    enc_ms = sorted(e[0].elapsed_time(e[1]) for e in evs)
+    dec_ms = sorted(e[1].elapsed_time(e[2]) for e in evs)
+    enc_avg = sum(enc_ms) / len(enc_ms)
+    dec_avg = sum(dec_ms) / len(dec_ms)
+    if world > 1:
+        t = torch.tensor([elapsed, enc_avg, dec_avg], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, enc_avg, dec_avg = t.tolist()
+
+    # PCIe-inclusive (host buffers, pinned) rate for DESIGN.md; rank 0 only.
+    e2e = None
+    if args.e2e and rank == 0:
+        e2e = e2e_rate(ks, pt, iv, L, tl, n, stream)
+
+    lib = _native.load()
+    n_cu = lib.rt_num_cus(_native.context(local))
+    peak_valu = n_cu * 128 * 2.4e9            # int32 lane-ops/s: 4 SIMD x 32 lanes per CU per clock
+    peak_lds = n_cu * 32 * 2.4e9              # ds_read_b32 lane-lookups/s (2 cycles per wave64 instr per CU)
+    ops_e, ops_d = ops_enc(L) * n, ops_dec(L) * n
+    dom = "decrypt" if dec_avg > enc_avg else "encrypt"
+    dom_ms = max(enc_avg, dec_avg)
+    dom_ops = ops_d if dom == "decrypt" else ops_e
+    achieved = dom_ops / (dom_ms * 1e-3)
+    bytes_enc = n * (L + 16 + tl + 0)         # read pt + iv, write token
+    bytes_dec = n * (tl + (tl - 48) + 8)      # read token, write pt + len + status
+    hbm_bytes = bytes_dec if dom == "decrypt" else bytes_enc
+
+    if world > 1:
+        dist.barrier()
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    cpu = cpu_baseline(args.cpu_seconds, args.cpu_workers, L) if world == 1 else None
+    pkts_total = n * world * args.steps
+    value = pkts_total / elapsed
+    line = {
+        "metric": "device-resident packets/s + GiB/s AES-256-CBC+HMAC-SHA256 at 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "packets/s",
+        "gib_s": value * L / 2**30,
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8/u32 (integer)",
+        "data": "synthetic uniform random plaintext and IVs generated on device (torch.randint), random keys",
+        "config": {"workload": ("c2: 2^20 x 500 B packets per GPU, single link key" if args.keys == 1 else
+                                f"c3: 2^20 x 500 B packets per GPU, {args.keys} per-packet keys")
+                   if (n == 1 << 20 and L == 500) else f"{n} x {L} B packets per GPU, {args.keys} key(s)",
+                   "packets_per_gpu": n, "plaintext_bytes": L, "token_bytes": tl, "keys": args.keys,
+                   "step": "encrypt+MAC then verify+decrypt of the same batch", "parallelism": f"shard{world}"},
+        "kernels": {
+            "encrypt": {"ms": enc_avg, "packets_s": n / (enc_avg * 1e-3),
+                        "gib_s": n * L / (enc_avg * 1e-3) / 2**30,
+                        "valu_frac": ops_e / (enc_avg * 1e-3) / peak_valu,
+                        "lds_frac": n * blocks(L) * LDS_LOOKUPS_PER_BLOCK / (enc_avg * 1e-3) / peak_lds},
+            "decrypt": {"ms": dec_avg, "packets_s": n / (dec_avg * 1e-3),
+                        "gib_s": n * L / (dec_avg * 1e-3) / 2**30,
+                        "valu_frac": ops_d / (dec_avg * 1e-3) / peak_valu,
+                        "lds_frac": n * blocks(L) * LDS_LOOKUPS_PER_BLOCK / (dec_avg * 1e-3) / peak_lds},
+        },
+        "roofline": {"bound": "valu", "kernel": dom, "achieved": achieved / 1e12, "peak": peak_valu / 1e12,
+                     "unit": "TOP/s", "frac": achieved / peak_valu, "traffic": None,
+                     "ops_per_packet": ops_dec(L) if dom == "decrypt" else ops_enc(L),
+                     "algorithmic_hbm_gb_s": hbm_bytes / (dom_ms * 1e-3) / 1e9,
+                     "note": "int32 VALU lane-ops (canonical model, SURVEY §8(d)) / HIP-event kernel time; "
+                             "peak = CUs x 128 lanes x 2.4 GHz; traffic from rocprofv3 PMC in profiles/"},
+        "cpu_baseline": cpu,
+        "e2e_pcie": e2e,
+    }
+    print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def e2e_rate(ks, pt_dev, iv_dev, L, tl, n, stream, reps=3):
+    """Host-memory in, host-memory out: pinned H2D of plaintext+IVs, encrypt,
+    D2H of tokens (and the mirror for decrypt), all on one stream."""
+    import torch
+    from reticulum_amd import device
+    pt_h = pt_dev.cpu().pin_memory()
+    iv_h = iv_dev.cpu().pin_memory()
+    tok_h = torch.empty((n, tl), dtype=torch.uint8).pin_memory()
+    back_h = torch.empty((n, tl - 48), dtype=torch.uint8).pin_memory()
+    pt_d, iv_d = torch.empty_like(pt_dev), torch.empty_like(iv_dev)
+    tok_d = torch.empty((n, tl), dtype=torch.uint8, device=pt_dev.device)
+    back_d = torch.empty((n, tl - 48), dtype=torch.uint8, device=pt_dev.device)
+    ol = torch.empty(n, dtype=torch.int32, device=pt_dev.device)
+    st = torch.empty(n, dtype=torch.int32, device=pt_dev.device)
+    times_e, times_d = [], []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pt_d.copy_(pt_h, non_blocking=True)
+        iv_d.copy_(iv_h, non_blocking=True)
+        device.encrypt_uniform(ks, pt_d, L, iv_d, tok_d, stream=stream)
+        tok_h.copy_(tok_d, non_blocking=True)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        tok_d.copy_(tok_h, non_blocking=True)
+        device.decrypt_uniform(ks, tok_d, tl, back_d, ol, st, stream=stream)
+        back_h.copy_(back_d, non_blocking=True)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        times_e.append(t1 - t0)
+        times_d.append(t2 - t1)
+    te, td = min(times_e), min(times_d)
+    return {"encrypt_packets_s": n / te, "decrypt_packets_s": n / td, "roundtrip_packets_s": n / (te + td),
+            "encrypt_gib_s": n * L / te / 2**30, "decrypt_gib_s": n * L / td / 2**30,
+            "note": "pinned host buffers, H2D + kernel + D2H serialised on one stream, best of %d" % reps}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,142 @@
+/*
+ * rnstok.h — C-ABI of the MI355X encrypted-token engine (librnstok.so).
+ *
+ * Drop-in boundary for Reticulum's per-packet token path.  The reference is
+ * pure Python; the maintainer-side binding is a ctypes stub
+ * behind the unchanged class surface of RNS/Cryptography/Token.py.  Each
+ * entry point names the reference interface it replaces (markqvist/Reticulum
+ * 1.4.2, paths relative to the repository root):
+ *
+ *   rt_keyset_create   Token.__init__            RNS/Cryptography/Token.py:58-74
+ *                      (+ the per-call key schedule AES.py:83,100 and the
+ *                       per-call HMAC key pad HMAC.py:73-82, hoisted per key)
+ *   rt_encrypt*        Token.encrypt             RNS/Cryptography/Token.py:87-97
+ *   rt_decrypt*        Token.verify_hmac+decrypt RNS/Cryptography/Token.py:77-84,100-114
+ *   rt_token_len       token size arithmetic     Token.py:50 (TOKEN_OVERHEAD) + PKCS7.py:35-39
+ *
+ * Conventions
+ *  - No exceptions cross the boundary.  API misuse returns a negative RT_E_*
+ *    code and sets a thread-local message (rt_last_error).  Per-packet
+ *    outcomes of decrypt are reported in an int32 status array (RT_ST_*),
+ *    mirroring the reference's exception classes (Token.py:78,102,114;
+ *    PKCS7.py:45-46): the Python layer maps non-zero status to ValueError.
+ *  - The caller owns every buffer; the library never frees caller memory.
+ *    rt_encrypt / rt_decrypt take DEVICE pointers and a hipStream_t (as
+ *    void*; NULL = HIP's null stream, which is also torch's default stream)
+ *    and only enqueue work.
+ *    rt_*_host take HOST pointers, stage through the context's workspace and
+ *    return after the results are back in host memory.
+ *  - Token layout (Token.py:96-97): iv(16) || AES-CBC(ek, iv, PKCS7(pt)) ||
+ *    HMAC-SHA256(sk, iv||ct)(32), so len(token) = 16 + 16*(L/16 + 1) + 32.
+ *  - Key layout (Token.py:61-70): 64-byte keys -> sk = key[0:32],
+ *    ek = key[32:64], AES-256-CBC; 32-byte keys -> sk = key[0:16],
+ *    ek = key[16:32], AES-128-CBC.  One keyset holds keys of one length.
+ *  - IVs are supplied by the caller (16 bytes per packet), drawn from
+ *    os.urandom as in Token.py:89; the library never generates IVs.
+ *  - Thread safety: a context may be used from several host threads; host
+ *    staging calls are serialised per context.  Device calls are re-entrant
+ *    given distinct output buffers.
+ */
+#ifndef RNSTOK_H
+#define RNSTOK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RNSTOK_ABI_VERSION 1
+
+/* Return codes (< 0: API misuse or runtime failure). */
+#define RT_OK        0
+#define RT_E_INVAL  -1   /* bad argument (NULL pointer, bad key length, ...) */
+#define RT_E_HIP    -2   /* HIP runtime error (message in rt_last_error)     */
+#define RT_E_NOMEM  -3   /* device or pinned allocation failed               */
+#define RT_E_NODEV  -4   /* no usable gfx950 device                          */
+
+/* Per-packet decrypt status. */
+#define RT_ST_OK          0  /* plaintext written, pt_len set                    */
+#define RT_ST_TOO_SHORT   1  /* len(token) <= 32            (Token.py:78)        */
+#define RT_ST_BAD_HMAC    2  /* tag mismatch                (Token.py:102)       */
+#define RT_ST_BAD_CT_LEN  3  /* valid tag, ct empty or %16  (Token.py:114 wrap)  */
+#define RT_ST_BAD_PAD     4  /* valid tag, last byte > 16   (PKCS7.py:45-46)     */
+
+typedef struct rt_ctx rt_ctx;
+typedef struct rt_keyset rt_keyset;
+
+/* ---- library / context --------------------------------------------------- */
+int         rt_abi_version(void);
+const char *rt_last_error(void);
+int         rt_device_count(void);
+/* One context per device.  Builds the S-box tables on the device. */
+rt_ctx     *rt_create(int device);
+void        rt_destroy(rt_ctx *ctx);
+/* Number of compute units the context launches over (persistent grid). */
+int         rt_num_cus(const rt_ctx *ctx);
+
+/* ---- keys (Token.__init__, Token.py:58-74) ------------------------------- */
+/* keys: HOST pointer, n_keys x key_len bytes, key_len 64 (AES-256) or 32
+ * (AES-128).  Runs the key-setup kernel: AES encryption and equivalent
+ * decryption schedules plus HMAC-SHA256 ipad/opad midstates per key. */
+rt_keyset  *rt_keyset_create(rt_ctx *ctx, const uint8_t *keys, uint32_t key_len, uint32_t n_keys);
+/* Same, with the raw keys already in DEVICE memory (on-device key tables). */
+rt_keyset  *rt_keyset_create_device(rt_ctx *ctx, const uint8_t *d_keys, uint32_t key_len, uint32_t n_keys,
+                                    void *stream);
+void        rt_keyset_destroy(rt_keyset *ks);
+uint32_t    rt_keyset_size(const rt_keyset *ks);
+
+/* ---- sizes --------------------------------------------------------------- */
+uint64_t    rt_token_len(uint64_t pt_len);      /* 16 + 16*(pt_len/16+1) + 32 */
+
+/* ---- device-resident batch (Token.encrypt over n packets) ---------------- */
+/* pt + pt_off[i] holds pt_len[i] plaintext bytes; key_idx[i] selects the key
+ * (NULL: key 0 for every packet); iv + 16*i is packet i's IV; the token is
+ * written at tok + tok_off[i] (rt_token_len(pt_len[i]) bytes).  Offsets need
+ * no alignment.  All pointers are device pointers. */
+int rt_encrypt(const rt_keyset *ks, const uint8_t *pt, const uint64_t *pt_off, const uint32_t *pt_len,
+               const uint32_t *key_idx, const uint8_t *iv, uint8_t *tok, const uint64_t *tok_off,
+               uint32_t n, void *stream);
+/* Fixed-length batch: packet i at pt + i*pt_stride (pt_len bytes), token at
+ * tok + i*tok_stride. */
+int rt_encrypt_uniform(const rt_keyset *ks, const uint8_t *pt, uint64_t pt_stride, uint32_t pt_len,
+                       const uint32_t *key_idx, const uint8_t *iv, uint8_t *tok, uint64_t tok_stride,
+                       uint32_t n, void *stream);
+
+/* ---- device-resident batch (Token.decrypt over n tokens) ----------------- */
+/* tok + tok_off[i] holds tok_len[i] token bytes; plaintext (up to
+ * tok_len[i]-48 bytes, including the pad block) is written at pt + pt_off[i];
+ * pt_len[i] receives the unpadded length on RT_ST_OK, the offending pad
+ * byte on RT_ST_BAD_PAD (authenticated data), 0 otherwise; status[i] one
+ * of RT_ST_*.  On any non-OK status the packet's plaintext region is zeroed
+ * (unauthenticated plaintext is never left behind). */
+int rt_decrypt(const rt_keyset *ks, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,
+               const uint32_t *key_idx, uint8_t *pt, const uint64_t *pt_off, uint32_t *pt_len,
+               int32_t *status, uint32_t n, void *stream);
+int rt_decrypt_uniform(const rt_keyset *ks, const uint8_t *tok, uint64_t tok_stride, uint32_t tok_len,
+                       const uint32_t *key_idx, uint8_t *pt, uint64_t pt_stride, uint32_t *pt_len,
+                       int32_t *status, uint32_t n, void *stream);
+
+/* ---- host-buffer convenience (PCIe-inclusive path) ----------------------- */
+/* Same meaning with HOST pointers; H2D, kernel, D2H on the context's stream,
+ * synchronised before return. */
+int rt_encrypt_host(const rt_keyset *ks, const uint8_t *pt, const uint64_t *pt_off, const uint32_t *pt_len,
+                    const uint32_t *key_idx, const uint8_t *iv, uint8_t *tok, const uint64_t *tok_off,
+                    uint32_t n);
+int rt_decrypt_host(const rt_keyset *ks, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,
+                    const uint32_t *key_idx, uint8_t *pt, const uint64_t *pt_off, uint32_t *pt_len,
+                    int32_t *status, uint32_t n);
+
+/* ---- memory helpers (so a non-torch host can drive the device API) ------- */
+void *rt_device_alloc(rt_ctx *ctx, uint64_t bytes);
+void  rt_device_free(rt_ctx *ctx, void *p);
+void *rt_host_alloc(uint64_t bytes);            /* pinned */
+void  rt_host_free(void *p);
+int   rt_memcpy_h2d(rt_ctx *ctx, void *dst, const void *src, uint64_t bytes, void *stream);
+int   rt_memcpy_d2h(rt_ctx *ctx, void *dst, const void *src, uint64_t bytes, void *stream);
+int   rt_stream_sync(rt_ctx *ctx, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RNSTOK_H */

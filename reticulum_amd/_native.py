@@ -1,0 +1,138 @@
+"""ctypes binding of librnstok.so (include/rnstok.h).
+
+The HIP library is the only compute path: if it is missing or no gfx950
+device is usable, every call raises :class:`NativeUnavailable` — there is no
+CPU fallback.
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librnstok.so")
+
+RT_OK, RT_E_INVAL, RT_E_HIP, RT_E_NOMEM, RT_E_NODEV = 0, -1, -2, -3, -4
+RT_ST_OK, RT_ST_TOO_SHORT, RT_ST_BAD_HMAC, RT_ST_BAD_CT_LEN, RT_ST_BAD_PAD = 0, 1, 2, 3, 4
+
+# (name, restype, argtypes) for every entry point declared in include/rnstok.h
+_vp, _u32, _u64, _i32, _int = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int
+SIGNATURES = [
+    ("rt_abi_version", _int, []),
+    ("rt_last_error", ctypes.c_char_p, []),
+    ("rt_device_count", _int, []),
+    ("rt_create", _vp, [_int]),
+    ("rt_destroy", None, [_vp]),
+    ("rt_num_cus", _int, [_vp]),
+    ("rt_keyset_create", _vp, [_vp, _vp, _u32, _u32]),
+    ("rt_keyset_create_device", _vp, [_vp, _vp, _u32, _u32, _vp]),
+    ("rt_keyset_destroy", None, [_vp]),
+    ("rt_keyset_size", _u32, [_vp]),
+    ("rt_token_len", _u64, [_u64]),
+    ("rt_encrypt", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),
+    ("rt_encrypt_uniform", _int, [_vp, _vp, _u64, _u32, _vp, _vp, _vp, _u64, _u32, _vp]),
+    ("rt_decrypt", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),
+    ("rt_decrypt_uniform", _int, [_vp, _vp, _u64, _u32, _vp, _vp, _u64, _vp, _vp, _u32, _vp]),
+    ("rt_encrypt_host", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32]),
+    ("rt_decrypt_host", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32]),
+    ("rt_device_alloc", _vp, [_vp, _u64]),
+    ("rt_device_free", None, [_vp, _vp]),
+    ("rt_host_alloc", _vp, [_u64]),
+    ("rt_host_free", None, [_vp]),
+    ("rt_memcpy_h2d", _int, [_vp, _vp, _vp, _u64, _vp]),
+    ("rt_memcpy_d2h", _int, [_vp, _vp, _vp, _u64, _vp]),
+    ("rt_stream_sync", _int, [_vp, _vp]),
+]
+
+
+class NativeUnavailable(RuntimeError):
+    """librnstok.so could not be loaded or no gfx950 device is usable."""
+
+
+class NativeError(RuntimeError):
+    """A librnstok call returned a negative RT_E_* code."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"librnstok error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def _share_hip_runtime_with_torch():
+    """One HIP runtime per process.
+
+    torch-ROCm ships its own libamdhip64 (soname libamdhip64.so.7, loaded from
+    torch/lib by name ``libamdhip64.so``); librnstok NEEDs libamdhip64.so.7.
+    Loading librnstok first would pull /opt/rocm's copy and torch would then
+    load a second runtime that finds no GPU.  When torch is installed, preload
+    its copy globally so librnstok binds to it and torch later reuses it."""
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is None or not spec.submodule_search_locations:
+        return
+    cand = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if os.path.exists(cand):
+        try:
+            ctypes.CDLL(os.path.realpath(cand), mode=ctypes.RTLD_GLOBAL)
+        except OSError:
+            pass
+
+
+def load():
+    """Load librnstok.so and bind every declared symbol (no GPU needed)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise NativeUnavailable(
+                    f"{LIB_PATH} not found: build it with `make -C reticulum_amd/csrc` "
+                    "(or __graft_entry__.build()); there is no CPU fallback")
+            _share_hip_runtime_with_torch()
+            try:
+                lib = ctypes.CDLL(LIB_PATH)
+            except OSError as e:
+                raise NativeUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+            for name, res, args in SIGNATURES:
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def last_error():
+    msg = load().rt_last_error()
+    return msg.decode(errors="replace") if msg else ""
+
+
+def check(rc):
+    if rc < 0:
+        raise NativeError(rc, last_error())
+    return rc
+
+
+_contexts = {}
+
+
+def context(device=None):
+    """Process-wide context for ``device`` (default: $RNSTOK_DEVICE or 0)."""
+    if device is None:
+        device = int(os.environ.get("RNSTOK_DEVICE", "0"))
+    ctx = _contexts.get(device)
+    if ctx is None:
+        lib = load()
+        with _lock:
+            ctx = _contexts.get(device)
+            if ctx is None:
+                ctx = lib.rt_create(device)
+                if not ctx:
+                    raise NativeUnavailable(f"rt_create({device}) failed: {last_error()}")
+                _contexts[device] = ctx
+    return ctx

@@ -1,0 +1,422 @@
+// token_capi.hip — C-ABI of librnstok.so (declared in include/rnstok.h).
+//
+// Host-side runtime around the kernels: device contexts, key tables, argument
+// validation, host staging for the PCIe-inclusive path.  No exceptions cross
+// the boundary; errors are negative RT_E_* codes plus rt_last_error().
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+
+#include "../../include/rnstok.h"
+#include "token_device.h"
+#include "token_launch.h"
+
+using namespace rnstok;
+
+struct rt_ctx {
+    int device = 0;
+    int n_cu = 0;
+    hipStream_t stream = nullptr;
+    uint8_t *d_sbox = nullptr;     // 512 B: S-box || inverse S-box
+    std::mutex mu;                 // serialises host-staging calls
+    uint8_t *d_work = nullptr;     // host-path workspace
+    uint64_t work_cap = 0;
+};
+
+struct rt_keyset {
+    rt_ctx *ctx = nullptr;
+    uint32_t key_len = 0, n_keys = 0;
+    int nr = 0;
+    uint32_t *d_rec = nullptr;
+};
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+static int hip_fail(hipError_t e, const char *what) {
+    return fail(RT_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+#define RT_HIP(call, what)                         \
+    do {                                           \
+        hipError_t e_ = (call);                    \
+        if (e_ != hipSuccess) return hip_fail(e_, what); \
+    } while (0)
+
+// S-box from its definition (FIPS-197 §5.1.1): GF(2^8) inverse then affine map.
+static void make_sbox(uint8_t s[256], uint8_t inv[256]) {
+    uint8_t exp[256], log[256];
+    uint8_t x = 1;
+    for (int i = 0; i < 255; ++i) {          // generator 3
+        exp[i] = x;
+        log[x] = (uint8_t)i;
+        x = (uint8_t)(x ^ (uint8_t)((x << 1) ^ ((x & 0x80) ? 0x1b : 0)));
+    }
+    for (int v = 0; v < 256; ++v) {
+        uint8_t b = v ? exp[(255 - log[v]) % 255] : 0;
+        uint8_t r = b;
+        for (int i = 0; i < 4; ++i) {
+            b = (uint8_t)((b << 1) | (b >> 7));
+            r ^= b;
+        }
+        r ^= 0x63;
+        s[v] = r;
+        inv[r] = (uint8_t)v;
+    }
+}
+
+// Device-API streams: the caller's hipStream_t; NULL is HIP's null stream
+// (torch's default stream), never the context's private staging stream.
+static hipStream_t pick(const rt_ctx *, void *stream) { return (hipStream_t)stream; }
+
+extern "C" {
+
+int rt_abi_version(void) { return RNSTOK_ABI_VERSION; }
+const char *rt_last_error(void) { return g_err.c_str(); }
+
+int rt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+rt_ctx *rt_create(int device) {
+    int n = rt_device_count();
+    if (device < 0 || device >= n) {
+        fail(RT_E_NODEV, "no HIP device " + std::to_string(device) + " (found " + std::to_string(n) + ")");
+        return nullptr;
+    }
+    hipDeviceProp_t prop;
+    if (hipSetDevice(device) != hipSuccess || hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        fail(RT_E_HIP, "hipGetDeviceProperties failed");
+        return nullptr;
+    }
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        fail(RT_E_NODEV, std::string("librnstok is built for gfx950, device is ") + prop.gcnArchName);
+        return nullptr;
+    }
+    static std::once_flag once;
+    static hipError_t cfg = hipSuccess;
+    std::call_once(once, [] { cfg = configure_kernels(); });
+    if (cfg != hipSuccess) {
+        hip_fail(cfg, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+        return nullptr;
+    }
+    rt_ctx *c = new rt_ctx();
+    c->device = device;
+    c->n_cu = prop.multiProcessorCount;
+    uint8_t tables[512];
+    make_sbox(tables, tables + 256);
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->d_sbox, 512) != hipSuccess ||
+        hipMemcpy(c->d_sbox, tables, 512, hipMemcpyHostToDevice) != hipSuccess) {
+        fail(RT_E_HIP, "context setup failed");
+        rt_destroy(c);
+        return nullptr;
+    }
+    return c;
+}
+
+void rt_destroy(rt_ctx *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    hipFree(c->d_sbox);
+    hipFree(c->d_work);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int rt_num_cus(const rt_ctx *c) { return c ? c->n_cu : 0; }
+
+uint64_t rt_token_len(uint64_t pt_len) { return 16u + 16u * (pt_len / 16u + 1u) + 32u; }
+
+rt_keyset *rt_keyset_create_device(rt_ctx *c, const uint8_t *d_keys, uint32_t key_len, uint32_t n_keys,
+                                   void *stream) {
+    if (!c || !d_keys || n_keys == 0) {
+        fail(RT_E_INVAL, "rt_keyset_create: null context/keys or zero keys");
+        return nullptr;
+    }
+    if (key_len != 64 && key_len != 32) {   // Token.py:72
+        fail(RT_E_INVAL, "Token key must be 128 or 256 bits, not " + std::to_string(key_len * 8));
+        return nullptr;
+    }
+    hipSetDevice(c->device);
+    rt_keyset *k = new rt_keyset();
+    k->ctx = c;
+    k->key_len = key_len;
+    k->n_keys = n_keys;
+    k->nr = key_len == 64 ? 14 : 10;
+    hipStream_t s = pick(c, stream);
+    if (hipMalloc(&k->d_rec, (uint64_t)n_keys * REC_WORDS * 4) != hipSuccess) {
+        fail(RT_E_NOMEM, "key table allocation failed");
+        delete k;
+        return nullptr;
+    }
+    hipError_t e = launch_key_setup(d_keys, key_len, n_keys, c->d_sbox, k->d_rec, s);
+    if (e != hipSuccess) {
+        hip_fail(e, "key setup launch");
+        rt_keyset_destroy(k);
+        return nullptr;
+    }
+    return k;
+}
+
+rt_keyset *rt_keyset_create(rt_ctx *c, const uint8_t *keys, uint32_t key_len, uint32_t n_keys) {
+    if (!c || !keys || n_keys == 0) {
+        fail(RT_E_INVAL, "rt_keyset_create: null context/keys or zero keys");
+        return nullptr;
+    }
+    hipSetDevice(c->device);
+    uint8_t *d_keys = nullptr;
+    const uint64_t bytes = (uint64_t)n_keys * key_len;
+    if (hipMalloc(&d_keys, bytes ? bytes : 1) != hipSuccess) {
+        fail(RT_E_NOMEM, "key upload allocation failed");
+        return nullptr;
+    }
+    rt_keyset *k = nullptr;
+    if (hipMemcpyAsync(d_keys, keys, bytes, hipMemcpyHostToDevice, c->stream) == hipSuccess)
+        k = rt_keyset_create_device(c, d_keys, key_len, n_keys, c->stream);
+    else
+        fail(RT_E_HIP, "key upload failed");
+    hipStreamSynchronize(c->stream);   // the raw keys are not kept on the device
+    hipFree(d_keys);
+    return k;
+}
+
+void rt_keyset_destroy(rt_keyset *k) {
+    if (!k) return;
+    hipSetDevice(k->ctx->device);
+    hipDeviceSynchronize();
+    hipFree(k->d_rec);
+    delete k;
+}
+
+uint32_t rt_keyset_size(const rt_keyset *k) { return k ? k->n_keys : 0; }
+
+static int check_keyset(const rt_keyset *k) {
+    if (!k || !k->ctx || !k->d_rec) return fail(RT_E_INVAL, "null keyset");
+    return RT_OK;
+}
+
+static int enc_common(const rt_keyset *k, EncArgs &a, void *stream) {
+    int rc = check_keyset(k);
+    if (rc) return rc;
+    if (a.n == 0) return RT_OK;
+    if (!a.pt || !a.iv || !a.tok) return fail(RT_E_INVAL, "rt_encrypt: null buffer");
+    a.rec = k->d_rec;
+    a.sbox = k->ctx->d_sbox;
+    RT_HIP(hipSetDevice(k->ctx->device), "hipSetDevice");
+    RT_HIP(launch_encrypt(a, k->nr, k->ctx->n_cu, pick(k->ctx, stream)), "encrypt launch");
+    return RT_OK;
+}
+
+static int dec_common(const rt_keyset *k, DecArgs &a, void *stream) {
+    int rc = check_keyset(k);
+    if (rc) return rc;
+    if (a.n == 0) return RT_OK;
+    if (!a.tok || !a.pt || !a.out_len || !a.status) return fail(RT_E_INVAL, "rt_decrypt: null buffer");
+    a.rec = k->d_rec;
+    a.sbox = k->ctx->d_sbox;
+    RT_HIP(hipSetDevice(k->ctx->device), "hipSetDevice");
+    RT_HIP(launch_decrypt(a, k->nr, k->ctx->n_cu, pick(k->ctx, stream)), "decrypt launch");
+    return RT_OK;
+}
+
+int rt_encrypt(const rt_keyset *k, const uint8_t *pt, const uint64_t *pt_off, const uint32_t *pt_len,
+               const uint32_t *key_idx, const uint8_t *iv, uint8_t *tok, const uint64_t *tok_off, uint32_t n,
+               void *stream) {
+    if (n && (!pt_off || !pt_len || !tok_off)) return fail(RT_E_INVAL, "rt_encrypt: null offset/length array");
+    EncArgs a{};
+    a.pt = pt; a.pt_off = pt_off; a.pt_len = pt_len; a.key_idx = key_idx; a.iv = iv;
+    a.tok = tok; a.tok_off = tok_off; a.n = n;
+    return enc_common(k, a, stream);
+}
+
+int rt_encrypt_uniform(const rt_keyset *k, const uint8_t *pt, uint64_t pt_stride, uint32_t pt_len,
+                       const uint32_t *key_idx, const uint8_t *iv, uint8_t *tok, uint64_t tok_stride, uint32_t n,
+                       void *stream) {
+    if (n > 1 && (pt_stride < pt_len || tok_stride < rt_token_len(pt_len)))
+        return fail(RT_E_INVAL, "rt_encrypt_uniform: stride smaller than packet/token");
+    EncArgs a{};
+    a.pt = pt; a.pt_stride = pt_stride; a.uni_len = pt_len; a.key_idx = key_idx; a.iv = iv;
+    a.tok = tok; a.tok_stride = tok_stride; a.n = n;
+    return enc_common(k, a, stream);
+}
+
+int rt_decrypt(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,
+               const uint32_t *key_idx, uint8_t *pt, const uint64_t *pt_off, uint32_t *pt_len, int32_t *status,
+               uint32_t n, void *stream) {
+    if (n && (!tok_off || !tok_len || !pt_off)) return fail(RT_E_INVAL, "rt_decrypt: null offset/length array");
+    DecArgs a{};
+    a.tok = tok; a.tok_off = tok_off; a.tok_len = tok_len; a.key_idx = key_idx; a.pt = pt; a.pt_off = pt_off;
+    a.out_len = pt_len; a.status = status; a.n = n;
+    return dec_common(k, a, stream);
+}
+
+int rt_decrypt_uniform(const rt_keyset *k, const uint8_t *tok, uint64_t tok_stride, uint32_t tok_len,
+                       const uint32_t *key_idx, uint8_t *pt, uint64_t pt_stride, uint32_t *pt_len, int32_t *status,
+                       uint32_t n, void *stream) {
+    if (n > 1 && (tok_stride < tok_len || (tok_len > 48 && pt_stride < tok_len - 48)))
+        return fail(RT_E_INVAL, "rt_decrypt_uniform: stride smaller than token/plaintext");
+    DecArgs a{};
+    a.tok = tok; a.tok_stride = tok_stride; a.uni_len = tok_len; a.key_idx = key_idx; a.pt = pt;
+    a.pt_stride = pt_stride; a.out_len = pt_len; a.status = status; a.n = n;
+    return dec_common(k, a, stream);
+}
+
+// ---------------------------------------------------------------- host path
+
+static int ensure_work(rt_ctx *c, uint64_t bytes) {
+    if (bytes <= c->work_cap) return RT_OK;
+    uint64_t cap = std::max<uint64_t>(bytes, c->work_cap * 2);
+    cap = (cap + 4095) & ~4095ull;
+    hipFree(c->d_work);
+    c->d_work = nullptr;
+    c->work_cap = 0;
+    if (hipMalloc(&c->d_work, cap) != hipSuccess) return fail(RT_E_NOMEM, "workspace allocation failed");
+    c->work_cap = cap;
+    return RT_OK;
+}
+
+static uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
+
+int rt_encrypt_host(const rt_keyset *k, const uint8_t *pt, const uint64_t *pt_off, const uint32_t *pt_len,
+                    const uint32_t *key_idx, const uint8_t *iv, uint8_t *tok, const uint64_t *tok_off, uint32_t n) {
+    int rc = check_keyset(k);
+    if (rc) return rc;
+    if (n == 0) return RT_OK;
+    if (!pt_off || !pt_len || !tok_off || !iv || !tok) return fail(RT_E_INVAL, "rt_encrypt_host: null argument");
+    uint64_t pt_ext = 0, tok_ext = 0, tok_sum = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (key_idx && key_idx[i] >= k->n_keys) return fail(RT_E_INVAL, "key_idx out of range");
+        pt_ext = std::max<uint64_t>(pt_ext, pt_off[i] + pt_len[i]);
+        const uint64_t tl = rt_token_len(pt_len[i]);
+        tok_ext = std::max<uint64_t>(tok_ext, tok_off[i] + tl);
+        tok_sum += tl;
+    }
+    if (pt_ext && !pt) return fail(RT_E_INVAL, "rt_encrypt_host: null plaintext");
+    rt_ctx *c = k->ctx;
+    std::lock_guard<std::mutex> g(c->mu);
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    const uint64_t o_pt = 0, o_tok = align16(o_pt + std::max<uint64_t>(pt_ext, 1)),
+                   o_iv = align16(o_tok + tok_ext), o_po = align16(o_iv + 16ull * n),
+                   o_pl = align16(o_po + 8ull * n), o_to = align16(o_pl + 4ull * n), o_ki = align16(o_to + 8ull * n),
+                   total = align16(o_ki + (key_idx ? 4ull * n : 0));
+    if ((rc = ensure_work(c, total))) return rc;
+    uint8_t *w = c->d_work;
+    hipStream_t s = c->stream;
+    if (pt_ext) RT_HIP(hipMemcpyAsync(w + o_pt, pt, pt_ext, hipMemcpyHostToDevice, s), "H2D pt");
+    if (tok_sum != tok_ext)   // gaps between tokens: keep the caller's bytes there
+        RT_HIP(hipMemcpyAsync(w + o_tok, tok, tok_ext, hipMemcpyHostToDevice, s), "H2D tok");
+    RT_HIP(hipMemcpyAsync(w + o_iv, iv, 16ull * n, hipMemcpyHostToDevice, s), "H2D iv");
+    RT_HIP(hipMemcpyAsync(w + o_po, pt_off, 8ull * n, hipMemcpyHostToDevice, s), "H2D pt_off");
+    RT_HIP(hipMemcpyAsync(w + o_pl, pt_len, 4ull * n, hipMemcpyHostToDevice, s), "H2D pt_len");
+    RT_HIP(hipMemcpyAsync(w + o_to, tok_off, 8ull * n, hipMemcpyHostToDevice, s), "H2D tok_off");
+    if (key_idx) RT_HIP(hipMemcpyAsync(w + o_ki, key_idx, 4ull * n, hipMemcpyHostToDevice, s), "H2D key_idx");
+    EncArgs a{};
+    a.pt = w + o_pt; a.pt_off = (const uint64_t *)(w + o_po); a.pt_len = (const uint32_t *)(w + o_pl);
+    a.key_idx = key_idx ? (const uint32_t *)(w + o_ki) : nullptr; a.iv = w + o_iv;
+    a.tok = w + o_tok; a.tok_off = (const uint64_t *)(w + o_to); a.n = n;
+    if ((rc = enc_common(k, a, s))) return rc;
+    RT_HIP(hipMemcpyAsync(tok, w + o_tok, tok_ext, hipMemcpyDeviceToHost, s), "D2H tok");
+    RT_HIP(hipStreamSynchronize(s), "stream sync");
+    return RT_OK;
+}
+
+int rt_decrypt_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,
+                    const uint32_t *key_idx, uint8_t *pt, const uint64_t *pt_off, uint32_t *pt_len, int32_t *status,
+                    uint32_t n) {
+    int rc = check_keyset(k);
+    if (rc) return rc;
+    if (n == 0) return RT_OK;
+    if (!tok_off || !tok_len || !pt_off || !pt_len || !status) return fail(RT_E_INVAL, "rt_decrypt_host: null argument");
+    uint64_t tok_ext = 0, pt_ext = 0, pt_sum = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (key_idx && key_idx[i] >= k->n_keys) return fail(RT_E_INVAL, "key_idx out of range");
+        tok_ext = std::max<uint64_t>(tok_ext, tok_off[i] + tok_len[i]);
+        const uint64_t pl = tok_len[i] > 48 ? tok_len[i] - 48 : 0;
+        pt_ext = std::max<uint64_t>(pt_ext, pt_off[i] + pl);
+        pt_sum += pl;
+    }
+    if ((tok_ext && !tok) || (pt_ext && !pt)) return fail(RT_E_INVAL, "rt_decrypt_host: null buffer");
+    rt_ctx *c = k->ctx;
+    std::lock_guard<std::mutex> g(c->mu);
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    const uint64_t o_tok = 0, o_pt = align16(std::max<uint64_t>(tok_ext, 1)), o_to = align16(o_pt + std::max<uint64_t>(pt_ext, 1)),
+                   o_tl = align16(o_to + 8ull * n), o_po = align16(o_tl + 4ull * n), o_ol = align16(o_po + 8ull * n),
+                   o_st = align16(o_ol + 4ull * n), o_ki = align16(o_st + 4ull * n),
+                   total = align16(o_ki + (key_idx ? 4ull * n : 0));
+    if ((rc = ensure_work(c, total))) return rc;
+    uint8_t *w = c->d_work;
+    hipStream_t s = c->stream;
+    if (tok_ext) RT_HIP(hipMemcpyAsync(w + o_tok, tok, tok_ext, hipMemcpyHostToDevice, s), "H2D tok");
+    if (pt_ext && pt_sum != pt_ext) RT_HIP(hipMemcpyAsync(w + o_pt, pt, pt_ext, hipMemcpyHostToDevice, s), "H2D pt");
+    RT_HIP(hipMemcpyAsync(w + o_to, tok_off, 8ull * n, hipMemcpyHostToDevice, s), "H2D tok_off");
+    RT_HIP(hipMemcpyAsync(w + o_tl, tok_len, 4ull * n, hipMemcpyHostToDevice, s), "H2D tok_len");
+    RT_HIP(hipMemcpyAsync(w + o_po, pt_off, 8ull * n, hipMemcpyHostToDevice, s), "H2D pt_off");
+    if (key_idx) RT_HIP(hipMemcpyAsync(w + o_ki, key_idx, 4ull * n, hipMemcpyHostToDevice, s), "H2D key_idx");
+    DecArgs a{};
+    a.tok = w + o_tok; a.tok_off = (const uint64_t *)(w + o_to); a.tok_len = (const uint32_t *)(w + o_tl);
+    a.key_idx = key_idx ? (const uint32_t *)(w + o_ki) : nullptr; a.pt = w + o_pt;
+    a.pt_off = (const uint64_t *)(w + o_po); a.out_len = (uint32_t *)(w + o_ol); a.status = (int32_t *)(w + o_st);
+    a.n = n;
+    if ((rc = dec_common(k, a, s))) return rc;
+    if (pt_ext) RT_HIP(hipMemcpyAsync(pt, w + o_pt, pt_ext, hipMemcpyDeviceToHost, s), "D2H pt");
+    RT_HIP(hipMemcpyAsync(pt_len, w + o_ol, 4ull * n, hipMemcpyDeviceToHost, s), "D2H pt_len");
+    RT_HIP(hipMemcpyAsync(status, w + o_st, 4ull * n, hipMemcpyDeviceToHost, s), "D2H status");
+    RT_HIP(hipStreamSynchronize(s), "stream sync");
+    return RT_OK;
+}
+
+// ------------------------------------------------------------------ memory
+
+void *rt_device_alloc(rt_ctx *c, uint64_t bytes) {
+    if (!c) return nullptr;
+    void *p = nullptr;
+    hipSetDevice(c->device);
+    if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) {
+        fail(RT_E_NOMEM, "hipMalloc failed");
+        return nullptr;
+    }
+    return p;
+}
+void rt_device_free(rt_ctx *c, void *p) {
+    if (c) hipSetDevice(c->device);
+    hipFree(p);
+}
+void *rt_host_alloc(uint64_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+        fail(RT_E_NOMEM, "hipHostMalloc failed");
+        return nullptr;
+    }
+    return p;
+}
+void rt_host_free(void *p) { hipHostFree(p); }
+int rt_memcpy_h2d(rt_ctx *c, void *dst, const void *src, uint64_t bytes, void *stream) {
+    if (!c) return fail(RT_E_INVAL, "null context");
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    RT_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, pick(c, stream)), "H2D");
+    return RT_OK;
+}
+int rt_memcpy_d2h(rt_ctx *c, void *dst, const void *src, uint64_t bytes, void *stream) {
+    if (!c) return fail(RT_E_INVAL, "null context");
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    RT_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, pick(c, stream)), "D2H");
+    return RT_OK;
+}
+int rt_stream_sync(rt_ctx *c, void *stream) {
+    if (!c) return fail(RT_E_INVAL, "null context");
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    RT_HIP(hipStreamSynchronize(pick(c, stream)), "stream sync");
+    return RT_OK;
+}
+
+}  // extern "C"

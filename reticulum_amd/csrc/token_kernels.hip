@@ -1,0 +1,448 @@
+// token_kernels.hip — HIP kernels for the encrypted-token path on gfx950.
+//
+//   k_key_setup  : per key, AES key expansion (aes256.py:146-175 / aes128.py),
+//                  equivalent-inverse-cipher schedule, HMAC ipad/opad midstates
+//                  (HMAC.py:73-84).  One lane per key.
+//   k_encrypt    : Token.encrypt (Token.py:87-97) — one packet per lane:
+//                  PKCS7 pad, AES-CBC (serial chain in VGPRs, T-tables in LDS),
+//                  HMAC-SHA256 over iv||ct interleaved with the chain (one
+//                  SHA-256 compression per four cipher blocks).
+//   k_decrypt    : Token.verify_hmac + Token.decrypt (Token.py:77-84,100-114) —
+//                  one token per lane: HMAC verify and CBC decrypt in one pass
+//                  over the token, lenient PKCS7 unpad (PKCS7.py:42-48).
+//
+// Launch shape: one 1024-thread (single key) or 512-thread (per-packet keys)
+// workgroup per CU, persistent over the batch; the LDS table image is built
+// once per workgroup.  See DESIGN.md.
+#include "token_device.h"
+#include "token_launch.h"
+
+namespace rnstok {
+
+// ------------------------------------------------------------ LDS tables --
+
+__device__ __forceinline__ uint32_t xt(uint32_t b) { return ((b << 1) ^ ((b & 0x80u) ? 0x1bu : 0u)) & 0xffu; }
+__device__ __forceinline__ uint32_t gmul(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+    for (int i = 0; i < 8; ++i) {
+        if (b & 1) p ^= a;
+        a = xt(a);
+        b >>= 1;
+    }
+    return p;
+}
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return n ? ((x << n) | (x >> (32 - n))) : x; }
+
+// T0[x] = {02*S, 01*S, 01*S, 03*S} (bytes = rows 0..3 of the column word)
+__device__ __forceinline__ uint32_t te0(const uint8_t *sbox, uint32_t x) {
+    uint32_t s = sbox[x], s2 = xt(s);
+    return s2 | (s << 8) | (s << 16) | ((s2 ^ s) << 24);
+}
+// Td0[x] = {0e*y, 09*y, 0d*y, 0b*y}, y = InvS[x]
+__device__ __forceinline__ uint32_t td0(const uint8_t *inv, uint32_t x) {
+    uint32_t y = inv[x];
+    return gmul(y, 14) | (gmul(y, 9) << 8) | (gmul(y, 13) << 16) | (gmul(y, 11) << 24);
+}
+
+template <bool DEC>
+__device__ void fill_tables(uint32_t *tab, const uint8_t *sbox, const uint8_t *inv) {
+    // regions 0,1: 32768 dwords; dword d -> region d>>14, row (d>>6)&255, table (d>>5)&1
+    for (uint32_t d = threadIdx.x; d < 32768u; d += blockDim.x) {
+        uint32_t x = (d >> 6) & 255u, t = ((d >> 14) << 1) | ((d >> 5) & 1u);
+        uint32_t v = DEC ? td0(inv, x) : te0(sbox, x);
+        tab[d] = rotl(v, 8 * (int)t);
+    }
+    if (DEC) {
+        for (uint32_t d = threadIdx.x; d < 8192u; d += blockDim.x)
+            tab[32768u + d] = (uint32_t)inv[d >> 5] * 0x01010101u;
+    }
+    __syncthreads();
+}
+
+// --------------------------------------------------------------- layout --
+
+struct Layout {
+    const uint64_t *off;   // per-packet offsets, or null: i * stride
+    uint64_t stride;
+    const uint32_t *len;   // per-packet lengths, or null: uniform
+    uint32_t uni;
+    __device__ __forceinline__ uint64_t o(uint32_t i) const { return off ? off[i] : (uint64_t)i * stride; }
+    __device__ __forceinline__ uint32_t l(uint32_t i) const { return len ? len[i] : uni; }
+};
+
+template <int NR, bool PERKEY>
+struct Keys {
+    uint32_t rk[4 * (NR + 1)];
+    __device__ __forceinline__ void load(const uint32_t *rec, int base) {
+        if (PERKEY) {
+#pragma unroll
+            for (int i = 0; i < NR + 1; ++i) {
+                u32x4 v = *(const u32x4 *)(rec + base + 4 * i);
+                rk[4 * i] = v.x; rk[4 * i + 1] = v.y; rk[4 * i + 2] = v.z; rk[4 * i + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4 * (NR + 1); ++i) rk[i] = rec[base + i];
+        }
+    }
+};
+
+__device__ __forceinline__ void load8(uint32_t d[8], const uint32_t *p) {
+    u32x4 a = *(const u32x4 *)p, b = *(const u32x4 *)(p + 4);
+    d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+}
+
+// PKCS7 pad block (PKCS7.py:35-39): r (< 16) payload bytes at p, then 16-r copies of 16-r.
+__device__ __forceinline__ u32x4 pad_block(const uint8_t *p, uint32_t r) {
+    uint32_t n = 16u - r, w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        uint32_t b = ((uint32_t)i < r) ? (uint32_t)p[i] : n;
+        w[i >> 2] |= b << (8 * (i & 3));
+    }
+    u32x4 v = {w[0], w[1], w[2], w[3]};
+    return v;
+}
+
+// --------------------------------------------------------------- encrypt --
+
+template <int NR, bool PERKEY>
+__global__ __launch_bounds__(PERKEY ? 512 : 1024) void k_encrypt(EncArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
+    fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);
+    const char *tab = (const char *)tab_u32;
+    const uint32_t lane = threadIdx.x & 31u;
+    const uint32_t lc = (4u * lane) | (1u << 16);
+
+    Keys<NR, PERKEY> K;
+    uint32_t ipad[8], opad[8];
+    if (!PERKEY) {
+        K.load(a.rec, REC_ENC);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { ipad[i] = a.rec[REC_IPAD + i]; opad[i] = a.rec[REC_OPAD + i]; }
+    }
+    const Layout in{a.pt_off, a.pt_stride, a.pt_len, a.uni_len};
+    const uint32_t nthreads = gridDim.x * blockDim.x;
+
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < a.n; p += nthreads) {
+        if (PERKEY) {
+            const uint32_t *r = a.rec + (uint64_t)a.key_idx[p] * REC_WORDS;
+            K.load(r, REC_ENC);
+            load8(ipad, r + REC_IPAD);
+            load8(opad, r + REC_OPAD);
+        }
+        const uint32_t L = in.l(p);
+        const uint8_t *P = a.pt + in.o(p);
+        uint8_t *O = a.tok + (a.tok_off ? a.tok_off[p] : (uint64_t)p * a.tok_stride);
+        const u32x4 iv = ld16(a.iv + 16ull * p);
+        st16(O, iv);
+        uint8_t *C = O + 16;
+
+        const uint32_t nfull = L >> 4, nq = nfull >> 2, tb = (nfull & 3u) + 1u;
+        uint32_t h[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) h[i] = ipad[i];
+        u32x4 prev = iv;
+        for (uint32_t q = 0; q < nq; ++q) {
+            const u32x4 p0 = ld16(P), p1 = ld16(P + 16), p2 = ld16(P + 32), p3 = ld16(P + 48);
+            const u32x4 c0 = aes_enc<NR>(p0 ^ prev, K.rk, lc, tab);
+            const u32x4 c1 = aes_enc<NR>(p1 ^ c0, K.rk, lc, tab);
+            const u32x4 c2 = aes_enc<NR>(p2 ^ c1, K.rk, lc, tab);
+            const u32x4 c3 = aes_enc<NR>(p3 ^ c2, K.rk, lc, tab);
+            st16(C, c0); st16(C + 16, c1); st16(C + 32, c2); st16(C + 48, c3);
+            uint32_t w[16];
+            sha_units(w, prev, c0, c1, c2);
+            sha256_compress(h, w);
+            prev = c3;
+            P += 64; C += 64;
+        }
+        // tail: tb (1..4) blocks, the last one carries the PKCS7 pad
+        u32x4 u0 = prev, u1 = prev, u2 = prev, u3 = prev, u4 = prev;
+        {
+            const u32x4 x0 = tb == 1 ? pad_block(P, L & 15u) : ld16(P);
+            u1 = aes_enc<NR>(x0 ^ u0, K.rk, lc, tab);
+            st16(C, u1);
+        }
+        if (tb > 1) {
+            const u32x4 x1 = tb == 2 ? pad_block(P + 16, L & 15u) : ld16(P + 16);
+            u2 = aes_enc<NR>(x1 ^ u1, K.rk, lc, tab);
+            st16(C + 16, u2);
+        }
+        if (tb > 2) {
+            const u32x4 x2 = tb == 3 ? pad_block(P + 32, L & 15u) : ld16(P + 32);
+            u3 = aes_enc<NR>(x2 ^ u2, K.rk, lc, tab);
+            st16(C + 32, u3);
+        }
+        if (tb > 3) {
+            const u32x4 x3 = pad_block(P + 48, L & 15u);
+            u4 = aes_enc<NR>(x3 ^ u3, K.rk, lc, tab);
+            st16(C + 48, u4);
+        }
+        const uint32_t tu = tb + 1;   // units left for the SHA tail (2..5)
+        const uint64_t bits = (uint64_t)(64u + 16u + 16u * (nfull + 1u)) * 8u;
+        if (tu >= 4) {
+            uint32_t w[16];
+            sha_units(w, u0, u1, u2, u3);
+            sha256_compress(h, w);
+            sha_final_units(h, tu - 4, u4, u4, u4, bits);
+        } else {
+            sha_final_units(h, tu, u0, u1, u2, bits);
+        }
+        uint32_t tag[8];
+        hmac_outer(tag, h, opad);
+        u32x4 t0 = {bswap(tag[0]), bswap(tag[1]), bswap(tag[2]), bswap(tag[3])};
+        u32x4 t1 = {bswap(tag[4]), bswap(tag[5]), bswap(tag[6]), bswap(tag[7])};
+        st16(C + 16 * tb, t0);
+        st16(C + 16 * tb + 16, t1);
+    }
+}
+
+// --------------------------------------------------------------- decrypt --
+
+template <int NR, bool PERKEY>
+__global__ __launch_bounds__(PERKEY ? 512 : 1024) void k_decrypt(DecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
+    fill_tables<true>(tab_u32, a.sbox, a.sbox + 256);
+    const char *tab = (const char *)tab_u32;
+    const uint32_t lane = threadIdx.x & 31u;
+    const uint32_t lc = (4u * lane) | (1u << 16);
+    const uint32_t lc2 = (8u * lane) | (4u << 16);
+
+    Keys<NR, PERKEY> K;
+    uint32_t ipad[8], opad[8];
+    if (!PERKEY) {
+        K.load(a.rec, REC_DEC);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { ipad[i] = a.rec[REC_IPAD + i]; opad[i] = a.rec[REC_OPAD + i]; }
+    }
+    const Layout in{a.tok_off, a.tok_stride, a.tok_len, a.uni_len};
+    const uint32_t nthreads = gridDim.x * blockDim.x;
+
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < a.n; p += nthreads) {
+        const uint32_t *r = a.rec;
+        if (PERKEY) {
+            r = a.rec + (uint64_t)a.key_idx[p] * REC_WORDS;
+            K.load(r, REC_DEC);
+            load8(ipad, r + REC_IPAD);
+            load8(opad, r + REC_OPAD);
+        }
+        const uint32_t T = in.l(p);
+        const uint8_t *Kt = a.tok + in.o(p);
+        uint8_t *O = a.pt + (a.pt_off ? a.pt_off[p] : (uint64_t)p * a.pt_stride);
+        int32_t st;
+        uint32_t outlen = 0;
+
+        if (T < 64u || ((T - 48u) & 15u)) {
+            // Malformed length (rare): decide TOO_SHORT / BAD_HMAC / BAD_CT_LEN
+            // exactly as Token.decrypt would, without touching the AES path.
+            if (T <= 32u) {
+                st = 1;
+            } else {
+                uint32_t h[8], tag[8];
+                for (int i = 0; i < 8; ++i) h[i] = ipad[i];
+                sha_bytes_after_ipad(h, Kt, T - 32u);
+                hmac_outer(tag, h, opad);
+                uint32_t diff = 0;
+                for (int i = 0; i < 32; ++i) diff |= (uint32_t)Kt[T - 32u + i] ^ ((tag[i >> 2] >> (24 - 8 * (i & 3))) & 0xffu);
+                st = diff ? 2 : 3;
+            }
+            if (T > 48u)   // caller's region holds T-48 bytes: zero it
+                for (uint32_t i = 0; i < T - 48u; ++i) O[i] = 0;
+        } else {
+            const uint32_t nb = (T - 48u) >> 4, nq = (nb - 1u) >> 2, tb = ((nb - 1u) & 3u) + 1u;
+            uint32_t h[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) h[i] = ipad[i];
+            u32x4 prev = ld16(Kt);
+            const uint8_t *C = Kt + 16;
+            uint8_t *D = O;
+            for (uint32_t q = 0; q < nq; ++q) {
+                const u32x4 c0 = ld16(C), c1 = ld16(C + 16), c2 = ld16(C + 32), c3 = ld16(C + 48);
+                st16(D, aes_dec<NR>(c0, K.rk, lc, lc2, tab) ^ prev);
+                st16(D + 16, aes_dec<NR>(c1, K.rk, lc, lc2, tab) ^ c0);
+                st16(D + 32, aes_dec<NR>(c2, K.rk, lc, lc2, tab) ^ c1);
+                st16(D + 48, aes_dec<NR>(c3, K.rk, lc, lc2, tab) ^ c2);
+                uint32_t w[16];
+                sha_units(w, prev, c0, c1, c2);
+                sha256_compress(h, w);
+                prev = c3;
+                C += 64; D += 64;
+            }
+            u32x4 u0 = prev, u1 = prev, u2 = prev, u3 = prev, u4 = prev, last;
+            u1 = ld16(C);
+            last = aes_dec<NR>(u1, K.rk, lc, lc2, tab) ^ u0;
+            st16(D, last);
+            if (tb > 1) {
+                u2 = ld16(C + 16);
+                last = aes_dec<NR>(u2, K.rk, lc, lc2, tab) ^ u1;
+                st16(D + 16, last);
+            }
+            if (tb > 2) {
+                u3 = ld16(C + 32);
+                last = aes_dec<NR>(u3, K.rk, lc, lc2, tab) ^ u2;
+                st16(D + 32, last);
+            }
+            if (tb > 3) {
+                u4 = ld16(C + 48);
+                last = aes_dec<NR>(u4, K.rk, lc, lc2, tab) ^ u3;
+                st16(D + 48, last);
+            }
+            const uint32_t tu = tb + 1;
+            const uint64_t bits = (uint64_t)(64u + 16u + 16u * nb) * 8u;
+            if (tu >= 4) {
+                uint32_t w[16];
+                sha_units(w, u0, u1, u2, u3);
+                sha256_compress(h, w);
+                sha_final_units(h, tu - 4, u4, u4, u4, bits);
+            } else {
+                sha_final_units(h, tu, u0, u1, u2, bits);
+            }
+            uint32_t tag[8];
+            hmac_outer(tag, h, opad);
+            const u32x4 r0 = ld16(C + 16 * tb), r1 = ld16(C + 16 * tb + 16);
+            const uint32_t diff = (r0.x ^ bswap(tag[0])) | (r0.y ^ bswap(tag[1])) | (r0.z ^ bswap(tag[2])) |
+                                  (r0.w ^ bswap(tag[3])) | (r1.x ^ bswap(tag[4])) | (r1.y ^ bswap(tag[5])) |
+                                  (r1.z ^ bswap(tag[6])) | (r1.w ^ bswap(tag[7]));
+            const uint32_t padn = last.w >> 24;     // PKCS7.unpad: n = data[-1]
+            st = diff ? 2 : (padn > 16u ? 4 : 0);
+            if (st == 0) {
+                outlen = 16u * nb - padn;
+            } else {
+                if (st == 4) outlen = padn;   // authenticated pad byte, for the error message
+
+                const u32x4 z = {0u, 0u, 0u, 0u};
+                for (uint32_t i = 0; i < nb; ++i) st16(O + 16 * i, z);
+            }
+        }
+        a.status[p] = st;
+        a.out_len[p] = outlen;
+    }
+}
+
+// ------------------------------------------------------------- key setup --
+
+__device__ __forceinline__ uint32_t sub_word(const uint8_t *sbox, uint32_t w) {
+    return (uint32_t)sbox[w & 255u] | ((uint32_t)sbox[(w >> 8) & 255u] << 8) |
+           ((uint32_t)sbox[(w >> 16) & 255u] << 16) | ((uint32_t)sbox[w >> 24] << 24);
+}
+__device__ __forceinline__ uint32_t inv_mix_word(uint32_t w) {
+    uint32_t a0 = w & 255u, a1 = (w >> 8) & 255u, a2 = (w >> 16) & 255u, a3 = w >> 24;
+    uint32_t b0 = gmul(a0, 14) ^ gmul(a1, 11) ^ gmul(a2, 13) ^ gmul(a3, 9);
+    uint32_t b1 = gmul(a1, 14) ^ gmul(a2, 11) ^ gmul(a3, 13) ^ gmul(a0, 9);
+    uint32_t b2 = gmul(a2, 14) ^ gmul(a3, 11) ^ gmul(a0, 13) ^ gmul(a1, 9);
+    uint32_t b3 = gmul(a3, 14) ^ gmul(a0, 11) ^ gmul(a1, 13) ^ gmul(a2, 9);
+    return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+}
+
+__global__ __launch_bounds__(256) void k_key_setup(const uint8_t *keys, uint32_t key_len, uint32_t n_keys,
+                                                    const uint8_t *sbox, uint32_t *rec_out) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_keys) return;
+    const uint8_t *key = keys + (uint64_t)k * key_len;
+    uint32_t *rec = rec_out + (uint64_t)k * REC_WORDS;
+    const uint32_t half = key_len / 2;          // sk = key[:half], ek = key[half:]  (Token.py:61-70)
+    const uint8_t *ek = key + half;
+    const int nk = (int)half / 4, nr = nk + 6, total = 4 * (nr + 1);
+    uint32_t w[60];
+    for (int i = 0; i < nk; ++i)
+        w[i] = (uint32_t)ek[4 * i] | ((uint32_t)ek[4 * i + 1] << 8) | ((uint32_t)ek[4 * i + 2] << 16) |
+               ((uint32_t)ek[4 * i + 3] << 24);
+    uint32_t rcon = 1;
+    for (int i = nk; i < total; ++i) {
+        uint32_t t = w[i - 1];
+        if (i % nk == 0) {
+            t = sub_word(sbox, (t >> 8) | (t << 24)) ^ rcon;    // RotWord then SubWord, Rcon in byte 0
+            rcon = xt(rcon);
+        } else if (nk > 6 && i % nk == 4) {
+            t = sub_word(sbox, t);
+        }
+        w[i] = w[i - nk] ^ t;
+    }
+    for (int i = 0; i < 60; ++i) rec[REC_ENC + i] = i < total ? w[i] : 0u;
+    // equivalent inverse cipher: dk[0] = rk[nr], dk[r] = InvMix(rk[nr-r]), dk[nr] = rk[0]
+    for (int r = 0; r <= nr; ++r)
+        for (int j = 0; j < 4; ++j) {
+            uint32_t v = w[4 * (nr - r) + j];
+            rec[REC_DEC + 4 * r + j] = (r == 0 || r == nr) ? v : inv_mix_word(v);
+        }
+    for (int i = 4 * (nr + 1); i < 60; ++i) rec[REC_DEC + i] = 0u;
+    // HMAC midstates (HMAC.py:73-82): sk zero-padded to 64 B, ^0x36 / ^0x5c
+    uint32_t blk[16], hi[8], ho[8];
+    const uint32_t iv0[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                             0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+    for (int pass = 0; pass < 2; ++pass) {
+        const uint32_t x = pass ? 0x5c5c5c5cu : 0x36363636u;
+        for (int i = 0; i < 16; ++i) {
+            uint32_t v = 0;
+            for (int b = 0; b < 4; ++b) {
+                uint32_t idx = 4 * i + b;
+                v = (v << 8) | (idx < half ? key[idx] : 0u);
+            }
+            blk[i] = v ^ x;
+        }
+        uint32_t *hs = pass ? ho : hi;
+        for (int i = 0; i < 8; ++i) hs[i] = iv0[i];
+        sha256_compress(hs, blk);
+    }
+    for (int i = 0; i < 8; ++i) { rec[REC_IPAD + i] = hi[i]; rec[REC_OPAD + i] = ho[i]; }
+}
+
+// --------------------------------------------------------------- launchers --
+
+template <int NR>
+static hipError_t launch_enc_nr(const EncArgs &a, int grid, hipStream_t s) {
+    if (a.key_idx) {
+        hipLaunchKernelGGL((k_encrypt<NR, true>), dim3(grid), dim3(512), LDS_ENC_BYTES, s, a);
+    } else {
+        hipLaunchKernelGGL((k_encrypt<NR, false>), dim3(grid), dim3(1024), LDS_ENC_BYTES, s, a);
+    }
+    return hipGetLastError();
+}
+template <int NR>
+static hipError_t launch_dec_nr(const DecArgs &a, int grid, hipStream_t s) {
+    if (a.key_idx) {
+        hipLaunchKernelGGL((k_decrypt<NR, true>), dim3(grid), dim3(512), LDS_DEC_BYTES, s, a);
+    } else {
+        hipLaunchKernelGGL((k_decrypt<NR, false>), dim3(grid), dim3(1024), LDS_DEC_BYTES, s, a);
+    }
+    return hipGetLastError();
+}
+
+static int grid_for(uint32_t n, int threads, int n_cu) {
+    uint64_t need = ((uint64_t)n + threads - 1) / threads;
+    uint64_t g = need < (uint64_t)n_cu ? need : (uint64_t)n_cu;
+    return g ? (int)g : 1;
+}
+
+hipError_t launch_encrypt(const EncArgs &a, int nr, int n_cu, hipStream_t s) {
+    const int g = grid_for(a.n, a.key_idx ? 512 : 1024, n_cu);
+    return nr == 14 ? launch_enc_nr<14>(a, g, s) : launch_enc_nr<10>(a, g, s);
+}
+hipError_t launch_decrypt(const DecArgs &a, int nr, int n_cu, hipStream_t s) {
+    const int g = grid_for(a.n, a.key_idx ? 512 : 1024, n_cu);
+    return nr == 14 ? launch_dec_nr<14>(a, g, s) : launch_dec_nr<10>(a, g, s);
+}
+hipError_t launch_key_setup(const uint8_t *keys, uint32_t key_len, uint32_t n_keys, const uint8_t *sbox,
+                            uint32_t *rec, hipStream_t s) {
+    hipLaunchKernelGGL(k_key_setup, dim3((n_keys + 255) / 256), dim3(256), 0, s, keys, key_len, n_keys, sbox, rec);
+    return hipGetLastError();
+}
+hipError_t configure_kernels() {
+    // 128 / 160 KiB of dynamic LDS per workgroup is above the default cap.
+    hipError_t e = hipSuccess;
+#define RT_CFG(k, bytes)                                                                                     \
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void *)(k), hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                                 (int)(bytes))
+    RT_CFG((k_encrypt<14, false>), LDS_ENC_BYTES);
+    RT_CFG((k_encrypt<14, true>), LDS_ENC_BYTES);
+    RT_CFG((k_encrypt<10, false>), LDS_ENC_BYTES);
+    RT_CFG((k_encrypt<10, true>), LDS_ENC_BYTES);
+    RT_CFG((k_decrypt<14, false>), LDS_DEC_BYTES);
+    RT_CFG((k_decrypt<14, true>), LDS_DEC_BYTES);
+    RT_CFG((k_decrypt<10, false>), LDS_DEC_BYTES);
+    RT_CFG((k_decrypt<10, true>), LDS_DEC_BYTES);
+#undef RT_CFG
+    return e;
+}
+
+}  // namespace rnstok

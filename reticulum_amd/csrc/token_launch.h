@@ -1,0 +1,47 @@
+// token_launch.h — internal interface between the C-ABI layer and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rnstok {
+
+struct EncArgs {
+    const uint32_t *rec;        // key records (REC_WORDS each)
+    const uint8_t *sbox;        // 256 B S-box || 256 B inverse S-box (device)
+    const uint8_t *pt;
+    const uint64_t *pt_off;     // null -> i * pt_stride
+    uint64_t pt_stride;
+    const uint32_t *pt_len;     // null -> uni_len
+    uint32_t uni_len;
+    const uint32_t *key_idx;    // null -> key 0
+    const uint8_t *iv;
+    uint8_t *tok;
+    const uint64_t *tok_off;    // null -> i * tok_stride
+    uint64_t tok_stride;
+    uint32_t n;
+};
+
+struct DecArgs {
+    const uint32_t *rec;
+    const uint8_t *sbox;
+    const uint8_t *tok;
+    const uint64_t *tok_off;
+    uint64_t tok_stride;
+    const uint32_t *tok_len;
+    uint32_t uni_len;
+    const uint32_t *key_idx;
+    uint8_t *pt;
+    const uint64_t *pt_off;
+    uint64_t pt_stride;
+    uint32_t *out_len;
+    int32_t *status;
+    uint32_t n;
+};
+
+hipError_t configure_kernels();
+hipError_t launch_encrypt(const EncArgs &a, int nr, int n_cu, hipStream_t s);
+hipError_t launch_decrypt(const DecArgs &a, int nr, int n_cu, hipStream_t s);
+hipError_t launch_key_setup(const uint8_t *keys, uint32_t key_len, uint32_t n_keys, const uint8_t *sbox,
+                            uint32_t *rec, hipStream_t s);
+
+}  // namespace rnstok

@@ -1,0 +1,76 @@
+"""Device-resident batch calls over torch tensors (the measured hot path).
+
+Thin wrappers over rt_encrypt* / rt_decrypt* (include/rnstok.h): every
+buffer is a CUDA(HIP) tensor already resident in HBM, the kernels are
+enqueued on the given stream (default: torch's current stream) and nothing is
+synchronised.  torch is used only for device memory and streams.
+"""
+import torch
+
+from . import _native
+from .token import KeySet
+
+
+def _p(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("device API needs tensors in device memory")
+    if not t.is_contiguous():
+        raise ValueError("device API needs contiguous tensors")
+    return t.data_ptr()
+
+
+def _stream(stream):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def _check_u8(*ts):
+    for t in ts:
+        if t is not None and t.dtype != torch.uint8:
+            raise ValueError("byte buffers must be torch.uint8")
+
+
+def encrypt_uniform(ks: KeySet, pt, pt_len, iv, tok, key_idx=None, stream=None):
+    """pt: (n, pt_stride) uint8; iv: (n, 16) uint8; tok: (n, tok_stride) uint8
+    with tok_stride >= token_len(pt_len); key_idx: (n,) int32 or None."""
+    _check_u8(pt, iv, tok)
+    n = pt.shape[0]
+    if iv.numel() < 16 * n or tok.shape[0] != n:
+        raise ValueError("shape mismatch")
+    if key_idx is not None and (key_idx.numel() != n or key_idx.dtype != torch.int32):
+        raise ValueError("key_idx must be (n,) int32")
+    lib = _native.load()
+    _native.check(lib.rt_encrypt_uniform(ks.handle, _p(pt), pt.stride(0), pt_len, _p(key_idx), _p(iv), _p(tok),
+                                         tok.stride(0), n, _stream(stream)))
+
+
+def decrypt_uniform(ks: KeySet, tok, tok_len, pt, out_len, status, key_idx=None, stream=None):
+    """tok: (n, tok_stride) uint8 holding tok_len-byte tokens; pt: (n, pt_stride)
+    uint8 with pt_stride >= tok_len - 48; out_len/status: (n,) int32."""
+    _check_u8(tok, pt)
+    n = tok.shape[0]
+    if pt.shape[0] != n or out_len.numel() != n or status.numel() != n:
+        raise ValueError("shape mismatch")
+    lib = _native.load()
+    _native.check(lib.rt_decrypt_uniform(ks.handle, _p(tok), tok.stride(0), tok_len, _p(key_idx), _p(pt),
+                                         pt.stride(0), _p(out_len), _p(status), n, _stream(stream)))
+
+
+def encrypt(ks: KeySet, pt, pt_off, pt_len, iv, tok, tok_off, key_idx=None, stream=None):
+    """Variable-length batch: pt/tok flat uint8 buffers, pt_off/tok_off int64,
+    pt_len int32, iv (n,16) uint8."""
+    _check_u8(pt, iv, tok)
+    n = pt_off.numel()
+    lib = _native.load()
+    _native.check(lib.rt_encrypt(ks.handle, _p(pt), _p(pt_off), _p(pt_len), _p(key_idx), _p(iv), _p(tok),
+                                 _p(tok_off), n, _stream(stream)))
+
+
+def decrypt(ks: KeySet, tok, tok_off, tok_len, pt, pt_off, out_len, status, key_idx=None, stream=None):
+    _check_u8(tok, pt)
+    n = tok_off.numel()
+    lib = _native.load()
+    _native.check(lib.rt_decrypt(ks.handle, _p(tok), _p(tok_off), _p(tok_len), _p(key_idx), _p(pt), _p(pt_off),
+                                 _p(out_len), _p(status), n, _stream(stream)))

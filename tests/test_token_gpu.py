@@ -1,0 +1,232 @@
+"""GPU parity tests: HIP kernels (through librnstok's C-ABI) vs the golden
+vectors generated from the reference and vs the C oracle on seeded batches.
+
+Bit-exact everywhere (integer/byte path).  Run with ``pytest -m gpu``.
+"""
+import numpy as np
+import pytest
+
+from oracle import ctoken as oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rt():
+    import reticulum_amd
+    from reticulum_amd import _native
+    lib = _native.load()
+    assert lib.rt_device_count() >= 1, "no HIP device visible"
+    _native.context(0)        # raises loudly if the HIP path is unusable
+    return reticulum_amd
+
+
+def _bytes(h):
+    return bytes.fromhex(h)
+
+
+def test_golden_encrypt_single_item(rt, golden):
+    """Token.encrypt with the reference's IV reproduces the reference token."""
+    for v in golden["encrypt"]:
+        ks = rt.KeySet(_bytes(v["key"]))
+        toks = ks.encrypt_batch([_bytes(v["pt"])], ivs=np.frombuffer(_bytes(v["iv"]), np.uint8))
+        assert toks[0].hex() == v["token"], (len(v["pt"]) // 2, v["key"][:8])
+
+
+def test_golden_encrypt_batched(rt, golden):
+    """All golden vectors of one key in one batch (unaligned packed offsets)."""
+    by_key = {}
+    for v in golden["encrypt"]:
+        by_key.setdefault(v["key"], []).append(v)
+    for key, vs in by_key.items():
+        ks = rt.KeySet(_bytes(key))
+        ivs = np.frombuffer(b"".join(_bytes(v["iv"]) for v in vs), np.uint8)
+        toks = ks.encrypt_batch([_bytes(v["pt"]) for v in vs], ivs=ivs)
+        assert [t.hex() for t in toks.to_list()] == [v["token"] for v in vs]
+        pts, st = ks.decrypt_batch(toks)
+        assert (st == 0).all()
+        assert [p.hex() for p in pts.to_list()] == [v["pt"] for v in vs]
+
+
+def test_golden_decrypt_cases(rt, golden):
+    """Negative/edge decrypt vectors: status and plaintext match the reference."""
+    for c in golden["decrypt"]:
+        ks = rt.KeySet(_bytes(c["key"]))
+        pts, st = ks.decrypt_batch([_bytes(c["token"])])
+        assert int(st[0]) == c["status"], c["name"]
+        if c["status"] == 0:
+            assert pts[0].hex() == c["pt"], c["name"]
+        else:
+            assert pts[0] == b"", c["name"]
+
+
+def test_golden_token_class_messages(rt, golden):
+    """Single-item Token raises the reference's exception class and message."""
+    for c in golden["decrypt"]:
+        t = rt.Token(_bytes(c["key"]))
+        tok = _bytes(c["token"])
+        if c["status"] == 0:
+            assert t.decrypt(tok).hex() == c["pt"]
+        else:
+            with pytest.raises(ValueError) as e:
+                t.decrypt(tok)
+            assert str(e.value) == c["msg"], c["name"]
+
+
+def test_reference_kat_fixed_token(rt, golden):
+    """tests/identity.py:157-158 KAT through the derived token key."""
+    k = golden["kat"]["fixed_token"]
+    t = rt.Token(_bytes(k["derived_key"]))
+    assert t.decrypt(_bytes(k["token"])).hex() == k["pt"]
+    assert t.verify_hmac(_bytes(k["token"]))
+
+
+def _random_batch(rng, n, lengths, n_keys, klen=64):
+    keys = rng.integers(0, 256, (n_keys, klen), dtype=np.uint8)
+    lens = np.asarray(lengths, dtype=np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    buf = rng.integers(0, 256, max(int(lens.sum()), 1), dtype=np.uint8)
+    ivs = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    kidx = rng.integers(0, n_keys, n, dtype=np.uint32) if n_keys > 1 else None
+    return keys, buf, off, lens, ivs, kidx
+
+
+def _oracle_tokens(keys, buf, off, lens, ivs, kidx):
+    n = len(off)
+    tl = (16 + 16 * (lens.astype(np.uint64) // 16 + 1) + 32).astype(np.uint32)
+    toff = np.zeros(n, np.uint64)
+    toff[1:] = np.cumsum(tl[:-1].astype(np.uint64))
+    tok = np.zeros(max(int(tl.astype(np.uint64).sum()), 1), np.uint8)
+    oracle.encrypt_batch(keys, buf, off, lens, kidx, ivs, tok, toff, threads=8)
+    return tok, toff, tl
+
+
+@pytest.mark.parametrize("klen", [64, 32])
+@pytest.mark.parametrize("n_keys", [1, 97])
+def test_random_lengths_vs_oracle(rt, klen, n_keys):
+    """Mixed lengths 0..4200 B, unaligned packing, single and per-packet keys,
+    AES-256 and AES-128 tokens: bit-exact vs the C oracle, and round trip."""
+    rng = np.random.Generator(np.random.PCG64(11 + klen + n_keys))
+    n = 3000
+    lens = rng.integers(0, 4200, n)
+    lens[:64] = np.arange(64)                 # every tail shape
+    keys, buf, off, lens, ivs, kidx = _random_batch(rng, n, lens, n_keys, klen)
+    tok, toff, tl = _oracle_tokens(keys, buf, off, lens, ivs, kidx)
+    ks = rt.KeySet(keys)
+    got = ks.encrypt_batch(rt.Packed(buf, off, lens), ivs=ivs, key_idx=kidx)
+    assert np.array_equal(got.length, tl)
+    assert np.array_equal(got.buf[:tok.size], tok[:got.buf.size])
+    pts, st = ks.decrypt_batch(got, key_idx=kidx)
+    assert (st == 0).all()
+    assert np.array_equal(pts.length, lens)
+    for i in range(0, n, 7):
+        assert pts[i] == buf[int(off[i]):int(off[i]) + int(lens[i])].tobytes()
+
+
+def test_tampered_tokens_exact_failures(rt):
+    """1 % tampered tokens (bit flips anywhere incl. tag): exactly those fail
+    with BAD_HMAC, the others decrypt; failed plaintext regions are zeroed."""
+    rng = np.random.Generator(np.random.PCG64(5))
+    n = 4096
+    keys, buf, off, lens, ivs, kidx = _random_batch(rng, n, rng.integers(64, 4097, n), 16)
+    ks = rt.KeySet(keys)
+    toks = ks.encrypt_batch(rt.Packed(buf, off, lens), ivs=ivs, key_idx=kidx)
+    bad = rng.random(n) < 0.01
+    for i in np.nonzero(bad)[0]:
+        pos = int(toks.off[i]) + int(rng.integers(0, int(toks.length[i])))
+        toks.buf[pos] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    pts, st = ks.decrypt_batch(toks, key_idx=kidx)
+    assert np.array_equal(st != 0, bad)
+    assert (st[bad] == rt.RT_ST_BAD_HMAC).all()
+    assert (pts.length[bad] == 0).all()
+
+
+def test_wrong_key_is_bad_hmac(rt):
+    ks1 = rt.KeySet(bytes(range(64)))
+    ks2 = rt.KeySet(bytes(range(1, 65)))
+    toks = ks1.encrypt_batch([b"x" * 100, b""])
+    _, st = ks2.decrypt_batch(toks)
+    assert list(st) == [rt.RT_ST_BAD_HMAC] * 2
+
+
+def test_device_uniform_full_size_round_trip(rt):
+    """Config c2 at full size (2^20 x 500 B, one key) through the device-resident
+    API: decrypt(encrypt(x)) == x, every status OK; a seeded sample of 2048
+    tokens is bit-exact vs the oracle."""
+    import torch
+    from reticulum_amd import device
+    n, L = 1 << 20, 500
+    tl = rt.token_len(L)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    pt = torch.randint(0, 256, (n, L), dtype=torch.uint8, device="cuda", generator=g)
+    iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
+    key = bytes(range(64))
+    ks = rt.KeySet(key)
+    tok = torch.empty((n, tl), dtype=torch.uint8, device="cuda")
+    device.encrypt_uniform(ks, pt, L, iv, tok)
+    back = torch.empty((n, tl - 48), dtype=torch.uint8, device="cuda")
+    out_len = torch.empty(n, dtype=torch.int32, device="cuda")
+    status = torch.empty(n, dtype=torch.int32, device="cuda")
+    device.decrypt_uniform(ks, tok, tl, back, out_len, status)
+    torch.cuda.synchronize()
+    assert int(status.abs().sum()) == 0
+    assert bool((out_len == L).all())
+    assert torch.equal(back[:, :L], pt)
+    idx = torch.randperm(n, generator=torch.Generator().manual_seed(3))[:2048].sort().values
+    s_pt = pt[idx.cuda()].cpu().numpy()
+    s_iv = iv[idx.cuda()].cpu().numpy()
+    s_tok = tok[idx.cuda()].cpu().numpy()
+    keys = np.frombuffer(key, np.uint8).reshape(1, 64)
+    lens = np.full(len(idx), L, np.uint32)
+    off = (np.arange(len(idx), dtype=np.uint64) * L)
+    ref, _, _ = _oracle_tokens(keys, s_pt.reshape(-1), off, lens, s_iv, None)
+    assert np.array_equal(ref.reshape(len(idx), tl), s_tok)
+
+
+def test_device_uniform_per_packet_keys(rt):
+    """Config c3 shape: 65 536 keys, uniform random key_idx, 500 B packets."""
+    import torch
+    from reticulum_amd import device
+    n, L, nk = 1 << 17, 500, 65536
+    tl = rt.token_len(L)
+    rng = np.random.Generator(np.random.PCG64(3))
+    keys = rng.integers(0, 256, (nk, 64), dtype=np.uint8)
+    ks = rt.KeySet(keys)
+    kidx = rng.integers(0, nk, n).astype(np.int32)
+    pt_h = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    iv_h = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    pt, iv, ki = torch.from_numpy(pt_h).cuda(), torch.from_numpy(iv_h).cuda(), torch.from_numpy(kidx).cuda()
+    tok = torch.empty((n, tl), dtype=torch.uint8, device="cuda")
+    device.encrypt_uniform(ks, pt, L, iv, tok, key_idx=ki)
+    back = torch.empty((n, tl - 48), dtype=torch.uint8, device="cuda")
+    out_len = torch.empty(n, dtype=torch.int32, device="cuda")
+    status = torch.empty(n, dtype=torch.int32, device="cuda")
+    device.decrypt_uniform(ks, tok, tl, back, out_len, status, key_idx=ki)
+    torch.cuda.synchronize()
+    assert int(status.abs().sum()) == 0
+    assert torch.equal(back[:, :L], pt)
+    sel = np.arange(0, n, 61)
+    off = np.arange(len(sel), dtype=np.uint64) * L
+    ref, _, _ = _oracle_tokens(keys, pt_h[sel].reshape(-1), off, np.full(len(sel), L, np.uint32), iv_h[sel],
+                               kidx[sel].astype(np.uint32))
+    assert np.array_equal(ref.reshape(len(sel), tl), tok.cpu().numpy()[sel])
+
+
+def test_resource_chunks_16k(rt):
+    """Config c4 shape (Resource-sized 16 KiB tokens), reduced count."""
+    import torch
+    from reticulum_amd import device
+    n, L = 4096, 16384
+    tl = rt.token_len(L)
+    rng = np.random.Generator(np.random.PCG64(4))
+    pt_h = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    iv_h = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    key = rng.integers(0, 256, 64, dtype=np.uint8)
+    ks = rt.KeySet(key.tobytes())
+    tok = torch.empty((n, tl), dtype=torch.uint8, device="cuda")
+    device.encrypt_uniform(ks, torch.from_numpy(pt_h).cuda(), L, torch.from_numpy(iv_h).cuda(), tok)
+    sel = np.arange(0, n, 97)
+    ref, _, _ = _oracle_tokens(key.reshape(1, 64), pt_h[sel].reshape(-1), np.arange(len(sel), dtype=np.uint64) * L,
+                               np.full(len(sel), L, np.uint32), iv_h[sel], None)
+    assert np.array_equal(ref.reshape(len(sel), tl), tok.cpu().numpy()[sel])

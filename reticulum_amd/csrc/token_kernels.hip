@@ -19,6 +19,18 @@
 
 namespace rnstok {
 
+// Workgroup sizes: one workgroup per CU (the LDS table image is 128/160 KiB).
+#ifndef RNSTOK_WG_ENC
+#define RNSTOK_WG_ENC 1024      // single key: 4 waves/SIMD, 128 VGPRs
+#endif
+#ifndef RNSTOK_WG_DEC
+#define RNSTOK_WG_DEC 1024
+#endif
+#ifndef RNSTOK_WG_PERKEY
+#define RNSTOK_WG_PERKEY 512    // per-packet keys: round keys live in VGPRs
+#endif
+constexpr int WG_ENC = RNSTOK_WG_ENC, WG_DEC = RNSTOK_WG_DEC, WG_PERKEY = RNSTOK_WG_PERKEY;
+
 // ------------------------------------------------------------ LDS tables --
 
 __device__ __forceinline__ uint32_t xt(uint32_t b) { return ((b << 1) ^ ((b & 0x80u) ? 0x1bu : 0u)) & 0xffu; }
@@ -81,11 +93,21 @@ struct Keys {
                 rk[4 * i] = v.x; rk[4 * i + 1] = v.y; rk[4 * i + 2] = v.z; rk[4 * i + 3] = v.w;
             }
         } else {
+            // one key for the whole launch: keep the schedule in SGPRs (VOP3
+            // operands), leaving the VGPR budget to the AES/SHA chains
 #pragma unroll
-            for (int i = 0; i < 4 * (NR + 1); ++i) rk[i] = rec[base + i];
+            for (int i = 0; i < 4 * (NR + 1); ++i) rk[i] = __builtin_amdgcn_readfirstlane(rec[base + i]);
         }
     }
 };
+
+// Uniform 8-word load re-issued per packet (scalar cache hit) instead of
+// being kept live in SGPRs across the packet loop.
+__device__ __forceinline__ void load_uniform8(uint32_t d[8], const uint32_t *p) {
+    asm volatile("" : "+s"(p));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = __builtin_amdgcn_readfirstlane(p[i]);
+}
 
 __device__ __forceinline__ void load8(uint32_t d[8], const uint32_t *p) {
     u32x4 a = *(const u32x4 *)p, b = *(const u32x4 *)(p + 4);
@@ -107,20 +129,17 @@ __device__ __forceinline__ u32x4 pad_block(const uint8_t *p, uint32_t r) {
 // --------------------------------------------------------------- encrypt --
 
 template <int NR, bool PERKEY>
-__global__ __launch_bounds__(PERKEY ? 512 : 1024) void k_encrypt(EncArgs a) {
+__global__ __launch_bounds__(PERKEY ? WG_PERKEY : WG_ENC) void k_encrypt(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
     fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);
-    const char *tab = (const char *)tab_u32;
-    const uint32_t lane = threadIdx.x & 31u;
-    const uint32_t lc = (4u * lane) | (1u << 16);
+#ifdef RNSTOK_SETPRIO
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= blockDim.x / 2) __builtin_amdgcn_s_setprio(1);
+#endif
+    const Lanes LN(threadIdx.x & 31u);
 
     Keys<NR, PERKEY> K;
     uint32_t ipad[8], opad[8];
-    if (!PERKEY) {
-        K.load(a.rec, REC_ENC);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) { ipad[i] = a.rec[REC_IPAD + i]; opad[i] = a.rec[REC_OPAD + i]; }
-    }
+    if (!PERKEY) K.load(a.rec, REC_ENC);
     const Layout in{a.pt_off, a.pt_stride, a.pt_len, a.uni_len};
     const uint32_t nthreads = gridDim.x * blockDim.x;
 
@@ -130,6 +149,9 @@ __global__ __launch_bounds__(PERKEY ? 512 : 1024) void k_encrypt(EncArgs a) {
             K.load(r, REC_ENC);
             load8(ipad, r + REC_IPAD);
             load8(opad, r + REC_OPAD);
+        } else {
+            load_uniform8(ipad, a.rec + REC_IPAD);
+            load_uniform8(opad, a.rec + REC_OPAD);
         }
         const uint32_t L = in.l(p);
         const uint8_t *P = a.pt + in.o(p);
@@ -142,42 +164,52 @@ __global__ __launch_bounds__(PERKEY ? 512 : 1024) void k_encrypt(EncArgs a) {
         uint32_t h[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) h[i] = ipad[i];
+        // Software pipeline: the SHA-256 compression of quad q-1's units is
+        // interleaved round by round with quad q's AES chain (enc_quad), so
+        // every wave carries an LDS-latency-bound and a VALU-bound chain.
         u32x4 prev = iv;
-        for (uint32_t q = 0; q < nq; ++q) {
-            const u32x4 p0 = ld16(P), p1 = ld16(P + 16), p2 = ld16(P + 32), p3 = ld16(P + 48);
-            const u32x4 c0 = aes_enc<NR>(p0 ^ prev, K.rk, lc, tab);
-            const u32x4 c1 = aes_enc<NR>(p1 ^ c0, K.rk, lc, tab);
-            const u32x4 c2 = aes_enc<NR>(p2 ^ c1, K.rk, lc, tab);
-            const u32x4 c3 = aes_enc<NR>(p3 ^ c2, K.rk, lc, tab);
-            st16(C, c0); st16(C + 16, c1); st16(C + 32, c2); st16(C + 48, c3);
-            uint32_t w[16];
-            sha_units(w, prev, c0, c1, c2);
-            sha256_compress(h, w);
-            prev = c3;
+        Sha256 S;                       // S.w: pending SHA block (previous quad's units)
+        u32x4 x[4], c[4];
+        if (nq > 0) {
+            x[0] = ld16(P); x[1] = ld16(P + 16); x[2] = ld16(P + 32); x[3] = ld16(P + 48);
+            enc_quad<NR, false>(c, x, prev, K.rk, LN, S);
+            st16(C, c[0]); st16(C + 16, c[1]); st16(C + 32, c[2]); st16(C + 48, c[3]);
+            sha_units(S.w, prev, c[0], c[1], c[2]);
+            prev = c[3];
             P += 64; C += 64;
         }
-        // tail: tb (1..4) blocks, the last one carries the PKCS7 pad
-        u32x4 u0 = prev, u1 = prev, u2 = prev, u3 = prev, u4 = prev;
+        for (uint32_t q = 1; q < nq; ++q) {
+            x[0] = ld16(P); x[1] = ld16(P + 16); x[2] = ld16(P + 32); x[3] = ld16(P + 48);
+            S.start(h);
+            enc_quad<NR, true>(c, x, prev, K.rk, LN, S);
+            S.finish(h);
+            st16(C, c[0]); st16(C + 16, c[1]); st16(C + 32, c[2]); st16(C + 48, c[3]);
+            sha_units(S.w, prev, c[0], c[1], c[2]);
+            prev = c[3];
+            P += 64; C += 64;
+        }
+        // tail: tb (1..4) blocks, the last one carries the PKCS7 pad; all four
+        // slots are computed (unused ones on zeros, never stored) so the
+        // pending compression can ride on the tail's AES chain.
         {
-            const u32x4 x0 = tb == 1 ? pad_block(P, L & 15u) : ld16(P);
-            u1 = aes_enc<NR>(x0 ^ u0, K.rk, lc, tab);
-            st16(C, u1);
+            const u32x4 z = {0u, 0u, 0u, 0u};
+            const uint32_t r = L & 15u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                x[j] = (uint32_t)j + 1u < tb ? ld16(P + 16 * j) : ((uint32_t)j + 1u == tb ? pad_block(P + 16 * j, r) : z);
         }
-        if (tb > 1) {
-            const u32x4 x1 = tb == 2 ? pad_block(P + 16, L & 15u) : ld16(P + 16);
-            u2 = aes_enc<NR>(x1 ^ u1, K.rk, lc, tab);
-            st16(C + 16, u2);
+        if (nq > 0) {
+            S.start(h);
+            enc_quad<NR, true>(c, x, prev, K.rk, LN, S);
+            S.finish(h);
+        } else {
+            enc_quad<NR, false>(c, x, prev, K.rk, LN, S);
         }
-        if (tb > 2) {
-            const u32x4 x2 = tb == 3 ? pad_block(P + 32, L & 15u) : ld16(P + 32);
-            u3 = aes_enc<NR>(x2 ^ u2, K.rk, lc, tab);
-            st16(C + 32, u3);
-        }
-        if (tb > 3) {
-            const u32x4 x3 = pad_block(P + 48, L & 15u);
-            u4 = aes_enc<NR>(x3 ^ u3, K.rk, lc, tab);
-            st16(C + 48, u4);
-        }
+        st16(C, c[0]);
+        if (tb > 1) st16(C + 16, c[1]);
+        if (tb > 2) st16(C + 32, c[2]);
+        if (tb > 3) st16(C + 48, c[3]);
+        const u32x4 u0 = prev, u1 = c[0], u2 = c[1], u3 = c[2], u4 = c[3];
         const uint32_t tu = tb + 1;   // units left for the SHA tail (2..5)
         const uint64_t bits = (uint64_t)(64u + 16u + 16u * (nfull + 1u)) * 8u;
         if (tu >= 4) {
@@ -200,21 +232,17 @@ __global__ __launch_bounds__(PERKEY ? 512 : 1024) void k_encrypt(EncArgs a) {
 // --------------------------------------------------------------- decrypt --
 
 template <int NR, bool PERKEY>
-__global__ __launch_bounds__(PERKEY ? 512 : 1024) void k_decrypt(DecArgs a) {
+__global__ __launch_bounds__(PERKEY ? WG_PERKEY : WG_DEC) void k_decrypt(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
     fill_tables<true>(tab_u32, a.sbox, a.sbox + 256);
-    const char *tab = (const char *)tab_u32;
-    const uint32_t lane = threadIdx.x & 31u;
-    const uint32_t lc = (4u * lane) | (1u << 16);
-    const uint32_t lc2 = (8u * lane) | (4u << 16);
+#ifdef RNSTOK_SETPRIO
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= blockDim.x / 2) __builtin_amdgcn_s_setprio(1);
+#endif
+    const Lanes LN(threadIdx.x & 31u);
 
     Keys<NR, PERKEY> K;
     uint32_t ipad[8], opad[8];
-    if (!PERKEY) {
-        K.load(a.rec, REC_DEC);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) { ipad[i] = a.rec[REC_IPAD + i]; opad[i] = a.rec[REC_OPAD + i]; }
-    }
+    if (!PERKEY) K.load(a.rec, REC_DEC);
     const Layout in{a.tok_off, a.tok_stride, a.tok_len, a.uni_len};
     const uint32_t nthreads = gridDim.x * blockDim.x;
 
@@ -225,6 +253,9 @@ __global__ __launch_bounds__(PERKEY ? 512 : 1024) void k_decrypt(DecArgs a) {
             K.load(r, REC_DEC);
             load8(ipad, r + REC_IPAD);
             load8(opad, r + REC_OPAD);
+        } else {
+            load_uniform8(ipad, a.rec + REC_IPAD);
+            load_uniform8(opad, a.rec + REC_OPAD);
         }
         const uint32_t T = in.l(p);
         const uint8_t *Kt = a.tok + in.o(p);
@@ -256,47 +287,46 @@ __global__ __launch_bounds__(PERKEY ? 512 : 1024) void k_decrypt(DecArgs a) {
             u32x4 prev = ld16(Kt);
             const uint8_t *C = Kt + 16;
             uint8_t *D = O;
+            Sha256 S;
+            u32x4 c[4], pp[4];
             for (uint32_t q = 0; q < nq; ++q) {
-                const u32x4 c0 = ld16(C), c1 = ld16(C + 16), c2 = ld16(C + 32), c3 = ld16(C + 48);
-                st16(D, aes_dec<NR>(c0, K.rk, lc, lc2, tab) ^ prev);
-                st16(D + 16, aes_dec<NR>(c1, K.rk, lc, lc2, tab) ^ c0);
-                st16(D + 32, aes_dec<NR>(c2, K.rk, lc, lc2, tab) ^ c1);
-                st16(D + 48, aes_dec<NR>(c3, K.rk, lc, lc2, tab) ^ c2);
-                uint32_t w[16];
-                sha_units(w, prev, c0, c1, c2);
-                sha256_compress(h, w);
-                prev = c3;
+                c[0] = ld16(C); c[1] = ld16(C + 16); c[2] = ld16(C + 32); c[3] = ld16(C + 48);
+                S.start(h);
+                sha_units(S.w, prev, c[0], c[1], c[2]);
+                dec_quad<NR, true>(pp, c, prev, K.rk, LN, S);
+                S.finish(h);
+                st16(D, pp[0]); st16(D + 16, pp[1]); st16(D + 32, pp[2]); st16(D + 48, pp[3]);
+                prev = c[3];
                 C += 64; D += 64;
             }
-            u32x4 u0 = prev, u1 = prev, u2 = prev, u3 = prev, u4 = prev, last;
-            u1 = ld16(C);
-            last = aes_dec<NR>(u1, K.rk, lc, lc2, tab) ^ u0;
-            st16(D, last);
-            if (tb > 1) {
-                u2 = ld16(C + 16);
-                last = aes_dec<NR>(u2, K.rk, lc, lc2, tab) ^ u1;
-                st16(D + 16, last);
+            // tail: tb (1..4) blocks; when tb >= 3 the units prev,c0,c1,c2 form a
+            // full SHA block, compressed inside the tail's AES chain.
+            {
+                const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) c[j] = (uint32_t)j < tb ? ld16(C + 16 * j) : z;
             }
-            if (tb > 2) {
-                u3 = ld16(C + 32);
-                last = aes_dec<NR>(u3, K.rk, lc, lc2, tab) ^ u2;
-                st16(D + 32, last);
+            const bool full = tb >= 3;
+            if (full) {
+                S.start(h);
+                sha_units(S.w, prev, c[0], c[1], c[2]);
+                dec_quad<NR, true>(pp, c, prev, K.rk, LN, S);
+                S.finish(h);
+            } else {
+                dec_quad<NR, false>(pp, c, prev, K.rk, LN, S);
             }
-            if (tb > 3) {
-                u4 = ld16(C + 48);
-                last = aes_dec<NR>(u4, K.rk, lc, lc2, tab) ^ u3;
-                st16(D + 48, last);
-            }
+            st16(D, pp[0]);
+            if (tb > 1) st16(D + 16, pp[1]);
+            if (tb > 2) st16(D + 32, pp[2]);
+            if (tb > 3) st16(D + 48, pp[3]);
+            const u32x4 last = tb == 1 ? pp[0] : (tb == 2 ? pp[1] : (tb == 3 ? pp[2] : pp[3]));
+            const u32x4 u0 = prev, u1 = c[0], u2 = c[1], u3 = c[2], u4 = c[3];
             const uint32_t tu = tb + 1;
             const uint64_t bits = (uint64_t)(64u + 16u + 16u * nb) * 8u;
-            if (tu >= 4) {
-                uint32_t w[16];
-                sha_units(w, u0, u1, u2, u3);
-                sha256_compress(h, w);
+            if (full)
                 sha_final_units(h, tu - 4, u4, u4, u4, bits);
-            } else {
+            else
                 sha_final_units(h, tu, u0, u1, u2, bits);
-            }
             uint32_t tag[8];
             hmac_outer(tag, h, opad);
             const u32x4 r0 = ld16(C + 16 * tb), r1 = ld16(C + 16 * tb + 16);
@@ -392,18 +422,18 @@ __global__ __launch_bounds__(256) void k_key_setup(const uint8_t *keys, uint32_t
 template <int NR>
 static hipError_t launch_enc_nr(const EncArgs &a, int grid, hipStream_t s) {
     if (a.key_idx) {
-        hipLaunchKernelGGL((k_encrypt<NR, true>), dim3(grid), dim3(512), LDS_ENC_BYTES, s, a);
+        hipLaunchKernelGGL((k_encrypt<NR, true>), dim3(grid), dim3(WG_PERKEY), LDS_ENC_BYTES, s, a);
     } else {
-        hipLaunchKernelGGL((k_encrypt<NR, false>), dim3(grid), dim3(1024), LDS_ENC_BYTES, s, a);
+        hipLaunchKernelGGL((k_encrypt<NR, false>), dim3(grid), dim3(WG_ENC), LDS_ENC_BYTES, s, a);
     }
     return hipGetLastError();
 }
 template <int NR>
 static hipError_t launch_dec_nr(const DecArgs &a, int grid, hipStream_t s) {
     if (a.key_idx) {
-        hipLaunchKernelGGL((k_decrypt<NR, true>), dim3(grid), dim3(512), LDS_DEC_BYTES, s, a);
+        hipLaunchKernelGGL((k_decrypt<NR, true>), dim3(grid), dim3(WG_PERKEY), LDS_DEC_BYTES, s, a);
     } else {
-        hipLaunchKernelGGL((k_decrypt<NR, false>), dim3(grid), dim3(1024), LDS_DEC_BYTES, s, a);
+        hipLaunchKernelGGL((k_decrypt<NR, false>), dim3(grid), dim3(WG_DEC), LDS_DEC_BYTES, s, a);
     }
     return hipGetLastError();
 }
@@ -415,11 +445,11 @@ static int grid_for(uint32_t n, int threads, int n_cu) {
 }
 
 hipError_t launch_encrypt(const EncArgs &a, int nr, int n_cu, hipStream_t s) {
-    const int g = grid_for(a.n, a.key_idx ? 512 : 1024, n_cu);
+    const int g = grid_for(a.n, a.key_idx ? WG_PERKEY : WG_ENC, n_cu);
     return nr == 14 ? launch_enc_nr<14>(a, g, s) : launch_enc_nr<10>(a, g, s);
 }
 hipError_t launch_decrypt(const DecArgs &a, int nr, int n_cu, hipStream_t s) {
-    const int g = grid_for(a.n, a.key_idx ? 512 : 1024, n_cu);
+    const int g = grid_for(a.n, a.key_idx ? WG_PERKEY : WG_DEC, n_cu);
     return nr == 14 ? launch_dec_nr<14>(a, g, s) : launch_dec_nr<10>(a, g, s);
 }
 hipError_t launch_key_setup(const uint8_t *keys, uint32_t key_len, uint32_t n_keys, const uint8_t *sbox,

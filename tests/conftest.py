@@ -4,8 +4,10 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-if ROOT not in sys.path:
-    sys.path.insert(0, ROOT)
+TESTS = os.path.join(ROOT, "tests")
+for p in (ROOT, TESTS):
+    if p not in sys.path:
+        sys.path.insert(0, p)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden", "token_vectors.json")
 

@@ -1,0 +1,110 @@
+"""CPU stand-in for librnstok's host-staging entry points — TEST ONLY.
+
+Implements rt_create / rt_keyset_* / rt_encrypt_host / rt_decrypt_host with
+the C oracle so the Python host layer (reticulum_amd.token: argument
+marshalling, key split, error mapping, Packed layout) can be unit-tested in
+the CPU suite.  It is installed only by tests (``install(monkeypatch)``); the
+product has no path to it, and the real kernels are covered by ``-m gpu``.
+"""
+import ctypes
+
+import numpy as np
+
+from oracle import ctoken
+
+
+def _arr(p, dtype, n):
+    if p is None:
+        return None
+    addr = p.value if isinstance(p, ctypes.c_void_p) else int(p)
+    if not addr or n == 0:
+        return np.zeros(0, dtype=dtype)
+    nbytes = np.dtype(dtype).itemsize * n
+    return np.frombuffer((ctypes.c_uint8 * nbytes).from_address(addr), dtype=dtype)
+
+
+class FakeLib:
+    def __init__(self):
+        self._keysets = {}
+        self._next = 1000
+        self.calls = []
+
+    def rt_last_error(self):
+        return b""
+
+    def rt_device_count(self):
+        return 1
+
+    def rt_create(self, device):
+        return 1
+
+    def rt_keyset_create(self, ctx, keys, klen, n):
+        if klen not in (32, 64):
+            return None
+        self._next += 1
+        self._keysets[self._next] = _arr(keys, np.uint8, klen * n).copy().reshape(n, klen)
+        return self._next
+
+    def rt_keyset_destroy(self, h):
+        self._keysets.pop(h, None)
+
+    def rt_encrypt_host(self, ks, pt, pt_off, pt_len, key_idx, iv, tok, tok_off, n):
+        self.calls.append(("encrypt", n))
+        keys = self._keysets[ks]
+        po, pl, to = _arr(pt_off, np.uint64, n), _arr(pt_len, np.uint32, n), _arr(tok_off, np.uint64, n)
+        ki = _arr(key_idx, np.uint32, n)
+        ivs = _arr(iv, np.uint8, 16 * n)
+        pext = int(max((po + pl).max(), 1))
+        text = int(max(to + 16 + 16 * (pl // 16 + 1) + 32))
+        pbuf, tbuf = _arr(pt, np.uint8, pext), _arr(tok, np.uint8, text)
+        for i in range(n):
+            k = keys[ki[i] if ki is not None else 0].tobytes()
+            t = ctoken.encrypt(k, ivs[16 * i:16 * i + 16].tobytes(), pbuf[po[i]:po[i] + pl[i]].tobytes())
+            tbuf[to[i]:to[i] + len(t)] = np.frombuffer(t, np.uint8)
+        return 0
+
+    def rt_decrypt_host(self, ks, tok, tok_off, tok_len, key_idx, pt, pt_off, pt_len, status, n):
+        self.calls.append(("decrypt", n))
+        keys = self._keysets[ks]
+        to, tl, po = _arr(tok_off, np.uint64, n), _arr(tok_len, np.uint32, n), _arr(pt_off, np.uint64, n)
+        ki = _arr(key_idx, np.uint32, n)
+        text = int(max((to + tl).max(), 1))
+        cap = np.where(tl > 48, tl.astype(np.int64) - 48, 0)
+        pext = int(max((po + cap).max(), 1))
+        tbuf, pbuf = _arr(tok, np.uint8, text), _arr(pt, np.uint8, pext)
+        ol, st = _arr(pt_len, np.uint32, n), _arr(status, np.int32, n)
+        for i in range(n):
+            k = keys[ki[i] if ki is not None else 0].tobytes()
+            t = tbuf[to[i]:to[i] + tl[i]].tobytes()
+            s, p = ctoken.decrypt(k, t)
+            st[i] = s
+            region = slice(int(po[i]), int(po[i] + cap[i]))
+            if s == 0:
+                pbuf[int(po[i]):int(po[i]) + len(p)] = np.frombuffer(p, np.uint8)
+                ol[i] = len(p)
+            else:
+                ol[i] = 0
+                if s == 4:          # the kernel reports the authenticated pad byte
+                    raw = _raw_last_byte(k, t)
+                    ol[i] = raw
+                pbuf[region] = 0
+        return 0
+
+
+def _raw_last_byte(key, tok):
+    """Last byte of the CBC-decrypted body (for BAD_PAD detail)."""
+    ek = key[len(key) // 2:]
+    last_ct, prev = tok[-48:-32], tok[-64:-48]
+    blk = ctoken.lib()
+    out = ctypes.create_string_buffer(16)
+    blk.oracle_aes_decrypt_block(ctypes.create_string_buffer(ek, len(ek)), len(ek),
+                                 ctypes.create_string_buffer(last_ct, 16), out)
+    return out.raw[15] ^ prev[15]
+
+
+def install(monkeypatch):
+    from reticulum_amd import _native
+    fake = FakeLib()
+    monkeypatch.setattr(_native, "_lib", fake)
+    monkeypatch.setattr(_native, "_contexts", {})
+    return fake

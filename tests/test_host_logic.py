@@ -1,0 +1,112 @@
+"""Host-layer tests of reticulum_amd.Token / KeySet / Packed on CPU.
+
+The HIP library is replaced by tests/fake_native.py (C oracle behind the same
+entry points) so that argument marshalling, the key split, the exception
+classes and messages of RNS/Cryptography/Token.py:58-114 are checked without
+a GPU.  The same assertions run against the real kernels in test_token_gpu.py.
+"""
+import numpy as np
+import pytest
+
+import reticulum_amd as rt
+from tests_helpers import b
+
+
+@pytest.fixture
+def fake(monkeypatch):
+    import fake_native
+    return fake_native.install(monkeypatch)
+
+
+def test_token_constants_and_generate_key():
+    assert rt.Token.TOKEN_OVERHEAD == 48
+    assert len(rt.Token.generate_key()) == 64
+    assert len(rt.Token.generate_key(rt.AES_128_CBC)) == 32
+    with pytest.raises(TypeError):
+        rt.Token.generate_key("bogus")
+
+
+def test_key_errors_match_reference(golden):
+    for e in golden["kat"]["key_errors"]:
+        key = None if e["key_len"] is None else bytes(e["key_len"])
+        with pytest.raises({"ValueError": ValueError, "TypeError": TypeError}[e["exc"]]) as ex:
+            rt.Token(key)
+        assert str(ex.value) == e["msg"]
+    with pytest.raises(TypeError):
+        rt.Token(bytes(64), mode="AES_9")
+
+
+def test_key_split(fake):
+    t = rt.Token(bytes(range(64)))
+    assert t.mode is rt.AES_256_CBC and t._signing_key == bytes(range(32)) and t._encryption_key == bytes(range(32, 64))
+    t = rt.Token(bytes(range(32)))
+    assert t.mode is rt.AES_128_CBC and t._signing_key == bytes(range(16))
+
+
+def test_type_errors_match_reference(golden, fake):
+    t = rt.Token(bytes(64))
+    for e in golden["kat"]["type_errors"]:
+        arg = bytearray(b"x") if e["arg_type"] == "bytearray" else "str"
+        with pytest.raises(TypeError) as ex:
+            getattr(t, e["method"])(arg)
+        assert str(ex.value) == e["msg"]
+    assert fake.calls == []          # rejected before reaching the library
+
+
+def test_golden_through_host_layer(golden, fake):
+    for v in golden["encrypt"][:60]:
+        ks = rt.KeySet(b(v["key"]))
+        toks = ks.encrypt_batch([b(v["pt"])], ivs=np.frombuffer(b(v["iv"]), np.uint8))
+        assert toks[0].hex() == v["token"]
+
+
+def test_decrypt_messages_through_host_layer(golden, fake):
+    for c in golden["decrypt"]:
+        t = rt.Token(b(c["key"]))
+        if c["status"] == 0:
+            assert t.decrypt(b(c["token"])).hex() == c["pt"]
+        else:
+            with pytest.raises(ValueError) as ex:
+                t.decrypt(b(c["token"]))
+            assert str(ex.value) == c["msg"], c["name"]
+
+
+def test_verify_hmac(golden, fake):
+    k = golden["kat"]["fixed_token"]
+    t = rt.Token(b(k["derived_key"]))
+    tok = b(k["token"])
+    assert t.verify_hmac(tok)
+    assert not t.verify_hmac(tok[:-1] + bytes([tok[-1] ^ 1]))
+    with pytest.raises(ValueError):
+        t.verify_hmac(bytes(32))
+
+
+def test_packed_layout_roundtrip(fake):
+    items = [b"", b"a", bytes(range(200)), b"z" * 17]
+    p = rt.Packed.from_list(items)
+    assert p.to_list() == items and list(p.off) == [0, 0, 1, 201]
+    ks = rt.KeySet([bytes(64), bytes(range(64))])
+    toks = ks.encrypt_batch(items, key_idx=[1, 0, 1, 0])
+    assert list(toks.length) == [rt.token_len(len(x)) for x in items]
+    back, st = ks.decrypt_batch(toks, key_idx=[1, 0, 1, 0])
+    assert list(st) == [0] * 4 and back.to_list() == items
+    _, st = ks.decrypt_batch(toks, key_idx=[0, 1, 0, 1])
+    assert list(st) == [rt.RT_ST_BAD_HMAC] * 4
+
+
+def test_batch_argument_validation(fake):
+    ks = rt.KeySet(bytes(64))
+    with pytest.raises(ValueError):
+        ks.encrypt_batch([b"x"], ivs=np.zeros(8, np.uint8))
+    with pytest.raises(ValueError):
+        ks.encrypt_batch([b"x"], key_idx=[3])
+    with pytest.raises(ValueError):
+        rt.KeySet([bytes(64), bytes(32)])
+    with pytest.raises(ValueError):
+        rt.KeySet(bytes(48))
+
+
+def test_fresh_iv_per_token(fake):
+    t = rt.Token(bytes(64))
+    a, c = t.encrypt(b"same"), t.encrypt(b"same")
+    assert a[:16] != c[:16] and t.decrypt(a) == t.decrypt(c) == b"same"

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Build an experimental librnstok variant: tools/build_variant.sh <name> <extra hipcc flags...>
+# Output: build_exp/<name>/librnstok.so  (load with tools/exp_bench.py)
+set -e
+NAME=$1; shift
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+mkdir -p $ROOT/build_exp/$NAME
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -w "$@" -shared -o $ROOT/build_exp/$NAME/librnstok.so \
+  $ROOT/reticulum_amd/csrc/token_kernels.hip $ROOT/reticulum_amd/csrc/token_capi.hip
+echo built build_exp/$NAME

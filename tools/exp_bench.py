@@ -1,0 +1,94 @@
+"""A/B timing of librnstok variants in ONE process, interleaved rounds.
+
+  python tools/exp_bench.py build_exp/a/librnstok.so build_exp/b/librnstok.so [--packets N] [--length L]
+
+Each variant is loaded with its own ctypes handle (RTLD_LOCAL), gets its own
+context and key set, and encrypts/decrypts the same device-resident batch;
+outputs are cross-checked between variants.  Prints median / min kernel ms.
+"""
+import argparse
+import ctypes
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--packets", type=int, default=1 << 20)
+    ap.add_argument("--length", type=int, default=500)
+    ap.add_argument("--rounds", type=int, default=15)
+    ap.add_argument("--keys", type=int, default=1)
+    args = ap.parse_args()
+
+    import torch
+    from reticulum_amd import _native
+    _native._share_hip_runtime_with_torch()
+    torch.cuda.init()
+
+    n, L = args.packets, args.length
+    tl = 16 + 16 * (L // 16 + 1) + 32
+    g = torch.Generator(device="cuda").manual_seed(1)
+    pt = torch.randint(0, 256, (n, L), dtype=torch.uint8, device="cuda", generator=g)
+    iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
+    keys = torch.randint(0, 256, (args.keys, 64), dtype=torch.uint8).numpy()
+    kidx = torch.randint(0, args.keys, (n,), dtype=torch.int32, device="cuda", generator=g) if args.keys > 1 else None
+    variants = []
+    for path in args.libs:
+        lib = ctypes.CDLL(os.path.abspath(path))
+        for name, res, argt in _native.SIGNATURES:
+            f = getattr(lib, name)
+            f.restype, f.argtypes = res, argt
+        ctx = lib.rt_create(0)
+        assert ctx, lib.rt_last_error()
+        ks = lib.rt_keyset_create(ctx, keys.ctypes.data_as(ctypes.c_void_p), 64, args.keys)
+        assert ks, lib.rt_last_error()
+        tok = torch.empty((n, tl), dtype=torch.uint8, device="cuda")
+        back = torch.empty((n, tl - 48), dtype=torch.uint8, device="cuda")
+        ol = torch.empty(n, dtype=torch.int32, device="cuda")
+        st = torch.empty(n, dtype=torch.int32, device="cuda")
+        variants.append(dict(path=path, lib=lib, ks=ks, tok=tok, back=back, ol=ol, st=st, enc=[], dec=[]))
+    s = torch.cuda.current_stream()
+    sp = s.cuda_stream
+    kp = kidx.data_ptr() if kidx is not None else None
+
+    def run(v, ev=None):
+        if ev:
+            ev[0].record(s)
+        rc = v["lib"].rt_encrypt_uniform(v["ks"], pt.data_ptr(), L, L, kp, iv.data_ptr(), v["tok"].data_ptr(), tl, n, sp)
+        assert rc == 0
+        if ev:
+            ev[1].record(s)
+        rc = v["lib"].rt_decrypt_uniform(v["ks"], v["tok"].data_ptr(), tl, tl, kp, v["back"].data_ptr(), tl - 48,
+                                         v["ol"].data_ptr(), v["st"].data_ptr(), n, sp)
+        assert rc == 0
+        if ev:
+            ev[2].record(s)
+
+    for v in variants:
+        run(v)
+        run(v)
+    torch.cuda.synchronize()
+    for v in variants:
+        ok = bool((v["st"] == 0).all()) and torch.equal(v["back"][:, :L], pt)
+        same = torch.equal(v["tok"], variants[0]["tok"])
+        print(f"{v['path']}: round-trip ok={ok} tokens==variant0: {same}")
+    for r in range(args.rounds):
+        for v in (variants if r % 2 == 0 else variants[::-1]):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            run(v, ev)
+            torch.cuda.synchronize()
+            v["enc"].append(ev[0].elapsed_time(ev[1]))
+            v["dec"].append(ev[1].elapsed_time(ev[2]))
+    for v in variants:
+        e, d = statistics.median(v["enc"]), statistics.median(v["dec"])
+        print(f"{v['path']:40s} enc {e:.4f} ms (min {min(v['enc']):.4f}) {n / e / 1e6:.3f} Gpkt/s | "
+              f"dec {d:.4f} ms (min {min(v['dec']):.4f}) {n / d / 1e6:.3f} Gpkt/s")
+
+
+if __name__ == "__main__":
+    main()

@@ -76,12 +76,18 @@ __device__ __forceinline__ u32x4 ld16(const uint8_t *p) {
 __device__ __forceinline__ void st16(uint8_t *p, u32x4 v) { __builtin_memcpy(p, &v, 16); }
 
 // Per-lane constants for LDS addressing; lane l always hits bank (l & 31).
+// A VALU op that reads an SGPR (or a constant materialised in one) issues at
+// half rate on gfx950 (tools/issue_probe.hip), so the byte mask of the hot
+// address computation is kept in a VGPR.
 struct Lanes {
     uint32_t r0;    // 4*lane            (region 0)
     uint32_t r1;    // 4*lane | 0x10000  (region 1; also the v_perm lane constant)
     uint32_t inv;   // 4*lane | 0x20000  (region 2, InvS rows of 128 B)
+    uint32_t m8;    // 0x0000ff00 in a VGPR
     __device__ __forceinline__ explicit Lanes(uint32_t lane)
-        : r0(4u * lane), r1(4u * lane | 0x10000u), inv(4u * lane | 0x20000u) {}
+        : r0(4u * lane), r1(4u * lane | 0x10000u), inv(4u * lane | 0x20000u), m8(0xff00u) {
+        asm volatile("" : "+v"(m8));
+    }
 };
 
 // ------------------------------------------------------------------ AES --
@@ -91,7 +97,7 @@ struct Lanes {
 // v_bitop3; bytes 0, 2, 3 take one (half-rate) v_perm_b32.
 template <int K, int REGION>
 __device__ __forceinline__ uint32_t taddr(uint32_t s, const Lanes &L) {
-    if (K == 1) return and_or(s, 0xff00u, REGION ? L.r1 : L.r0);
+    if (K == 1) return and_or(s, L.m8, REGION ? L.r1 : L.r0);
     return perm(s, L.r1, REGION ? Sel<K>::R1 : Sel<K>::R0);
 }
 

@@ -11,7 +11,7 @@
 //                  one token per lane: HMAC verify and CBC decrypt in one pass
 //                  over the token, lenient PKCS7 unpad (PKCS7.py:42-48).
 //
-// Launch shape: one 1024-thread (single key) or 512-thread (per-packet keys)
+// Launch shape: one 1024-thread (single key) or 768/512-thread (per-packet keys)
 // workgroup per CU, persistent over the batch; the LDS table image is built
 // once per workgroup.  See DESIGN.md.
 #include "token_device.h"
@@ -26,10 +26,15 @@ namespace rnstok {
 #ifndef RNSTOK_WG_DEC
 #define RNSTOK_WG_DEC 1024
 #endif
-#ifndef RNSTOK_WG_PERKEY
-#define RNSTOK_WG_PERKEY 512    // per-packet keys: round keys live in VGPRs
+// per-packet keys: the round keys live in VGPRs, so fewer waves per SIMD
+#ifndef RNSTOK_WG_PERKEY_ENC
+#define RNSTOK_WG_PERKEY_ENC 768   // <= 168 VGPRs, 3 waves/SIMD
 #endif
-constexpr int WG_ENC = RNSTOK_WG_ENC, WG_DEC = RNSTOK_WG_DEC, WG_PERKEY = RNSTOK_WG_PERKEY;
+#ifndef RNSTOK_WG_PERKEY_DEC
+#define RNSTOK_WG_PERKEY_DEC 512   // <= 256 VGPRs, 2 waves/SIMD (4 blocks in flight)
+#endif
+constexpr int WG_ENC = RNSTOK_WG_ENC, WG_DEC = RNSTOK_WG_DEC;
+constexpr int WG_PERKEY_ENC = RNSTOK_WG_PERKEY_ENC, WG_PERKEY_DEC = RNSTOK_WG_PERKEY_DEC;
 
 // ------------------------------------------------------------ LDS tables --
 
@@ -129,7 +134,7 @@ __device__ __forceinline__ u32x4 pad_block(const uint8_t *p, uint32_t r) {
 // --------------------------------------------------------------- encrypt --
 
 template <int NR, bool PERKEY>
-__global__ __launch_bounds__(PERKEY ? WG_PERKEY : WG_ENC) void k_encrypt(EncArgs a) {
+__global__ __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encrypt(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
     fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);
 #ifdef RNSTOK_SETPRIO
@@ -232,7 +237,7 @@ __global__ __launch_bounds__(PERKEY ? WG_PERKEY : WG_ENC) void k_encrypt(EncArgs
 // --------------------------------------------------------------- decrypt --
 
 template <int NR, bool PERKEY>
-__global__ __launch_bounds__(PERKEY ? WG_PERKEY : WG_DEC) void k_decrypt(DecArgs a) {
+__global__ __launch_bounds__(PERKEY ? WG_PERKEY_DEC : WG_DEC) void k_decrypt(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
     fill_tables<true>(tab_u32, a.sbox, a.sbox + 256);
 #ifdef RNSTOK_SETPRIO
@@ -419,38 +424,48 @@ __global__ __launch_bounds__(256) void k_key_setup(const uint8_t *keys, uint32_t
 
 // --------------------------------------------------------------- launchers --
 
-template <int NR>
-static hipError_t launch_enc_nr(const EncArgs &a, int grid, hipStream_t s) {
-    if (a.key_idx) {
-        hipLaunchKernelGGL((k_encrypt<NR, true>), dim3(grid), dim3(WG_PERKEY), LDS_ENC_BYTES, s, a);
-    } else {
-        hipLaunchKernelGGL((k_encrypt<NR, false>), dim3(grid), dim3(WG_ENC), LDS_ENC_BYTES, s, a);
-    }
-    return hipGetLastError();
-}
-template <int NR>
-static hipError_t launch_dec_nr(const DecArgs &a, int grid, hipStream_t s) {
-    if (a.key_idx) {
-        hipLaunchKernelGGL((k_decrypt<NR, true>), dim3(grid), dim3(WG_PERKEY), LDS_DEC_BYTES, s, a);
-    } else {
-        hipLaunchKernelGGL((k_decrypt<NR, false>), dim3(grid), dim3(WG_DEC), LDS_DEC_BYTES, s, a);
-    }
-    return hipGetLastError();
+// Launch shape: a persistent grid of at most one workgroup per CU (the table
+// image owns the CU's LDS).  Small batches (e.g. 16 KiB Resource tokens
+// sharded 8 ways) shrink the workgroup instead of the grid so that every CU
+// gets packets: threads = clamp(ceil(n / n_cu) rounded to a wave, 64, max).
+struct Shape {
+    int grid, threads;
+};
+static Shape shape_for(uint32_t n, int max_threads, int n_cu) {
+    const uint64_t per_cu = ((uint64_t)n + n_cu - 1) / n_cu;
+    uint64_t t = (per_cu + 63) / 64 * 64;
+    if (t < 64) t = 64;
+    if (t > (uint64_t)max_threads) t = max_threads;
+    uint64_t g = ((uint64_t)n + t - 1) / t;
+    if (g > (uint64_t)n_cu) g = n_cu;
+    if (g < 1) g = 1;
+    return {(int)g, (int)t};
 }
 
-static int grid_for(uint32_t n, int threads, int n_cu) {
-    uint64_t need = ((uint64_t)n + threads - 1) / threads;
-    uint64_t g = need < (uint64_t)n_cu ? need : (uint64_t)n_cu;
-    return g ? (int)g : 1;
+template <int NR>
+static hipError_t launch_enc_nr(const EncArgs &a, Shape sh, hipStream_t s) {
+    if (a.key_idx)
+        hipLaunchKernelGGL((k_encrypt<NR, true>), dim3(sh.grid), dim3(sh.threads), LDS_ENC_BYTES, s, a);
+    else
+        hipLaunchKernelGGL((k_encrypt<NR, false>), dim3(sh.grid), dim3(sh.threads), LDS_ENC_BYTES, s, a);
+    return hipGetLastError();
+}
+template <int NR>
+static hipError_t launch_dec_nr(const DecArgs &a, Shape sh, hipStream_t s) {
+    if (a.key_idx)
+        hipLaunchKernelGGL((k_decrypt<NR, true>), dim3(sh.grid), dim3(sh.threads), LDS_DEC_BYTES, s, a);
+    else
+        hipLaunchKernelGGL((k_decrypt<NR, false>), dim3(sh.grid), dim3(sh.threads), LDS_DEC_BYTES, s, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_encrypt(const EncArgs &a, int nr, int n_cu, hipStream_t s) {
-    const int g = grid_for(a.n, a.key_idx ? WG_PERKEY : WG_ENC, n_cu);
-    return nr == 14 ? launch_enc_nr<14>(a, g, s) : launch_enc_nr<10>(a, g, s);
+    const Shape sh = shape_for(a.n, a.key_idx ? WG_PERKEY_ENC : WG_ENC, n_cu);
+    return nr == 14 ? launch_enc_nr<14>(a, sh, s) : launch_enc_nr<10>(a, sh, s);
 }
 hipError_t launch_decrypt(const DecArgs &a, int nr, int n_cu, hipStream_t s) {
-    const int g = grid_for(a.n, a.key_idx ? WG_PERKEY : WG_DEC, n_cu);
-    return nr == 14 ? launch_dec_nr<14>(a, g, s) : launch_dec_nr<10>(a, g, s);
+    const Shape sh = shape_for(a.n, a.key_idx ? WG_PERKEY_DEC : WG_DEC, n_cu);
+    return nr == 14 ? launch_dec_nr<14>(a, sh, s) : launch_dec_nr<10>(a, sh, s);
 }
 hipError_t launch_key_setup(const uint8_t *keys, uint32_t key_len, uint32_t n_keys, const uint8_t *sbox,
                             uint32_t *rec, hipStream_t s) {

@@ -24,13 +24,15 @@ __global__ __launch_bounds__(1024) void k(uint32_t *out, uint32_t seed, int iter
 #pragma unroll
     for (int j = 0; j < 16; ++j) x[j] = (threadIdx.x * 977u + j * 131u) & 0xff00u;
     uint32_t v0 = threadIdx.x ^ seed, v1 = v0 * 3, v2 = v0 * 5, v3 = v0 * 7, v4 = v0 * 11, v5 = v0 * 13, v6 = v0 * 17, v7 = v0 * 19;
-    const uint32_t c1 = seed * 7 + 1, c2 = seed * 11 + 3;
+    uint32_t c1 = seed * 7 + 1 + threadIdx.x, c2 = seed * 11 + 3;
+    uint32_t mask = 0xff00u;
+    asm volatile("" : "+v"(c1), "+v"(c2), "+v"(mask));   // VGPR operands (SGPR operands halve VALU rate)
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
         for (int j = 0; j < LDS_PER_ITER; ++j) {
             uint32_t a;
             if (PERM) a = __builtin_amdgcn_perm(x[j & 15], lane, 0x0C0C0500u);
-            else a = (x[j & 15] & 0xff00u) | lane;
+            else a = __builtin_amdgcn_bitop3_b32(x[j & 15], mask, lane, 0xEA);
             x[j & 15] ^= *(l32 *)(uintptr_t)(a + ((j & 1) ? 128 : 0));
         }
 #pragma unroll
@@ -82,6 +84,7 @@ int main() {
     uint32_t *out;
     CHECK(hipMalloc(&out, 4ull * ncu * 1024));
     run<16, 0, false>("lds16 (and_or addr)", out, ncu, iters);
+    run<16, 16, false>("lds16 + valu16", out, ncu, iters);
     run<0, 64, false>("valu64 bitop3", out, ncu, iters);
     run<16, 64, false>("lds16 + valu64", out, ncu, iters);
     run<0, 32, false>("valu32 bitop3", out, ncu, iters);

@@ -249,17 +249,43 @@ def main():
                         "lds_frac": n * blocks(L) * LDS_LOOKUPS_PER_BLOCK / (dec_avg * 1e-3) / peak_lds},
         },
         "roofline": {"bound": "valu", "kernel": dom, "achieved": achieved / 1e12, "peak": peak_valu / 1e12,
-                     "unit": "TOP/s", "frac": achieved / peak_valu, "traffic": None,
+                     "unit": "TOP/s", "frac": achieved / peak_valu,
+                     "traffic": traffic_from_profiles(dom, n, L, args.keys),
                      "ops_per_packet": ops_dec(L) if dom == "decrypt" else ops_enc(L),
+                     "algorithmic_bytes_per_launch": hbm_bytes,
                      "algorithmic_hbm_gb_s": hbm_bytes / (dom_ms * 1e-3) / 1e9,
-                     "note": "int32 VALU lane-ops (canonical model, SURVEY §8(d)) / HIP-event kernel time; "
-                             "peak = CUs x 128 lanes x 2.4 GHz; traffic from rocprofv3 PMC in profiles/"},
+                     "frac_of_survey_P": achieved / (n_cu * 64 * 2.4e9),
+                     "lds_frac": n * blocks(L) * LDS_LOOKUPS_PER_BLOCK / (dom_ms * 1e-3) / peak_lds,
+                     "note": "achieved = canonical int32 VALU lane-ops per launch (SURVEY §8(d): 352/AES block, "
+                             "1464/SHA-256 compression, +8 tag compare) / HIP-event kernel time; peak = CUs x 128 "
+                             "lanes x 2.4 GHz (full-rate VALU); frac_of_survey_P uses BASELINE.md §5's P = CUs x 64 "
+                             "x 2.4 GHz; traffic = HBM bytes per launch from the committed rocprofv3 PMC summary "
+                             "(profiles/*_pmc.json, FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM)"},
         "cpu_baseline": cpu,
         "e2e_pcie": e2e,
     }
     print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def traffic_from_profiles(kernel, n, L, keys):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    whose workload matches (profiles/<round>_pmc.json, tools/pmc_summary.py)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    for path in reversed(files):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        meta = d.get("_workload", {})
+        if meta.get("packets") == n and meta.get("length") == L and meta.get("keys") == keys and kernel in d:
+            v = d[kernel].get("hbm_bytes_per_launch")
+            if v:
+                return {"bytes": v, "source": os.path.relpath(path, ROOT)}
+    return None
 
 
 def e2e_rate(ks, pt_dev, iv_dev, L, tl, n, stream, reps=3):

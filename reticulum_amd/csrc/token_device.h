@@ -109,6 +109,33 @@ __device__ __forceinline__ uint32_t tcol(uint32_t a, uint32_t b, uint32_t c, uin
                 lds(taddr<3, 1>(d, L), 128), k);
 }
 
+// A round split in two so independent work can sit between the LDS reads and
+// their use: tround_load issues the 16 lookups, tround_mix folds them.
+// Column j reads bytes 0..3 of words (j, j+1, j+2, j+3) for encryption and
+// (j, j-1, j-2, j-3) for the equivalent inverse cipher.
+template <bool DEC>
+__device__ __forceinline__ void tround_load(uint32_t v[16], const uint32_t s[4], const Lanes &L) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int i1 = DEC ? (j + 3) & 3 : (j + 1) & 3, i2 = (j + 2) & 3, i3 = DEC ? (j + 1) & 3 : (j + 3) & 3;
+        v[4 * j + 0] = lds(taddr<0, 0>(s[j], L), 0);
+        v[4 * j + 1] = lds(taddr<1, 0>(s[i1], L), 128);
+        v[4 * j + 2] = lds(taddr<2, 1>(s[i2], L), 0);
+        v[4 * j + 3] = lds(taddr<3, 1>(s[i3], L), 128);
+    }
+}
+__device__ __forceinline__ void tround_mix(uint32_t s[4], const uint32_t v[16], const uint32_t *k) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[j] = xor3(xor3(v[4 * j], v[4 * j + 1], v[4 * j + 2]), v[4 * j + 3], k[j]);
+}
+
+// Scheduling fence: the compiler may not move instructions across it.
+#ifndef RNSTOK_NO_SCHED_FENCE
+#define RT_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define RT_FENCE() ((void)0)
+#endif
+
 // Encryption final round column: row r from the table whose byte r is S[x]
 // (row0 <- T2, row1 <- T3, row2 <- T0, row3 <- T1), merged by byte masks.
 __device__ __forceinline__ uint32_t tlast_enc(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k,
@@ -269,16 +296,19 @@ __device__ __forceinline__ void enc_quad(u32x4 c[4], const u32x4 x[4], u32x4 cha
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
         const u32x4 in = x[b] ^ (b == 0 ? chain : c[b - 1]);
-        uint32_t s0 = in.x ^ rk[0], s1 = in.y ^ rk[1], s2 = in.z ^ rk[2], s3 = in.w ^ rk[3];
+        uint32_t st[4] = {in.x ^ rk[0], in.y ^ rk[1], in.z ^ rk[2], in.w ^ rk[3]};
 #pragma unroll
         for (int r = 1; r < NR; ++r) {
-            const uint32_t t0 = tcol(s0, s1, s2, s3, rk[4 * r + 0], L);
-            const uint32_t t1 = tcol(s1, s2, s3, s0, rk[4 * r + 1], L);
-            const uint32_t t2 = tcol(s2, s3, s0, s1, rk[4 * r + 2], L);
-            const uint32_t t3 = tcol(s3, s0, s1, s2, rk[4 * r + 3], L);
-            s0 = t0; s1 = t1; s2 = t2; s3 = t3;
-            if (WITH_SHA) S.round(b * NR + r - 1);
+            uint32_t v[16];
+            tround_load<false>(v, st, L);      // 16 LDS lookups in flight ...
+            if (WITH_SHA) {
+                RT_FENCE();
+                S.round(b * NR + r - 1);        // ... while one SHA-256 round issues
+                RT_FENCE();
+            }
+            tround_mix(st, v, rk + 4 * r);
         }
+        const uint32_t s0 = st[0], s1 = st[1], s2 = st[2], s3 = st[3];
         c[b].x = tlast_enc(s0, s1, s2, s3, rk[4 * NR + 0], L);
         c[b].y = tlast_enc(s1, s2, s3, s0, rk[4 * NR + 1], L);
         c[b].z = tlast_enc(s2, s3, s0, s1, rk[4 * NR + 2], L);
@@ -307,12 +337,14 @@ __device__ __forceinline__ void dec_quad(u32x4 p[4], const u32x4 c[4], u32x4 cha
     for (int r = 1; r < NR; ++r) {
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-            const uint32_t t0 = tcol(s[b][0], s[b][3], s[b][2], s[b][1], dk[4 * r + 0], L);
-            const uint32_t t1 = tcol(s[b][1], s[b][0], s[b][3], s[b][2], dk[4 * r + 1], L);
-            const uint32_t t2 = tcol(s[b][2], s[b][1], s[b][0], s[b][3], dk[4 * r + 2], L);
-            const uint32_t t3 = tcol(s[b][3], s[b][2], s[b][1], s[b][0], dk[4 * r + 3], L);
-            s[b][0] = t0; s[b][1] = t1; s[b][2] = t2; s[b][3] = t3;
-            if (WITH_SHA) S.round((r - 1) * 4 + b);
+            uint32_t v[16];
+            tround_load<true>(v, s[b], L);
+            if (WITH_SHA) {
+                RT_FENCE();
+                S.round((r - 1) * 4 + b);
+                RT_FENCE();
+            }
+            tround_mix(s[b], v, dk + 4 * r);
         }
     }
 #pragma unroll

@@ -34,6 +34,13 @@ namespace rnstok {
 #define RNSTOK_WG_PERKEY_DEC 512   // <= 256 VGPRs, 2 waves/SIMD (4 blocks in flight)
 #endif
 constexpr int WG_ENC = RNSTOK_WG_ENC, WG_DEC = RNSTOK_WG_DEC;
+// Optional explicit occupancy target (waves per SIMD) for the single-key
+// kernels, so the scheduler may spend registers on loads in flight.
+#ifdef RNSTOK_WAVES_PER_EU
+#define RT_OCC __attribute__((amdgpu_waves_per_eu(RNSTOK_WAVES_PER_EU, RNSTOK_WAVES_PER_EU)))
+#else
+#define RT_OCC
+#endif
 constexpr int WG_PERKEY_ENC = RNSTOK_WG_PERKEY_ENC, WG_PERKEY_DEC = RNSTOK_WG_PERKEY_DEC;
 
 // ------------------------------------------------------------ LDS tables --
@@ -134,7 +141,7 @@ __device__ __forceinline__ u32x4 pad_block(const uint8_t *p, uint32_t r) {
 // --------------------------------------------------------------- encrypt --
 
 template <int NR, bool PERKEY>
-__global__ __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encrypt(EncArgs a) {
+__global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encrypt(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
     fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);
 #ifdef RNSTOK_SETPRIO
@@ -237,7 +244,7 @@ __global__ __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encrypt(Enc
 // --------------------------------------------------------------- decrypt --
 
 template <int NR, bool PERKEY>
-__global__ __launch_bounds__(PERKEY ? WG_PERKEY_DEC : WG_DEC) void k_decrypt(DecArgs a) {
+__global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_DEC : WG_DEC) void k_decrypt(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
     fill_tables<true>(tab_u32, a.sbox, a.sbox + 256);
 #ifdef RNSTOK_SETPRIO

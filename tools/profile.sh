@@ -15,4 +15,10 @@ for PASS in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD 
   N=$(echo $PASS | tr ' ' '_' | cut -c1-40)
   timeout -k 10 300 rocprofv3 --pmc $PASS --output-format csv -d $OUT/pmc_$N -o run -- python3 bench.py $ARGS > $OUT/pmc_$N.log 2>&1 || { echo "pmc pass $N failed rc=$?"; tail -5 $OUT/pmc_$N.log; exit 1; }
 done
+WL=$(python3 -c "
+import sys; a=sys.argv[1:]
+g=lambda f,d: a[a.index(f)+1] if f in a else d
+print(','.join([g('--packets','1048576'), g('--length','500'), g('--keys','1')]))" $ARGS)
+python3 tools/pmc_summary.py $OUT --json $OUT/pmc.json --workload $WL > $OUT/pmc_summary.txt
+cp $OUT/trace/run_kernel_stats.csv $OUT/kernel_stats.csv
 echo profile done

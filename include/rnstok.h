@@ -117,6 +117,22 @@ int rt_decrypt_uniform(const rt_keyset *ks, const uint8_t *tok, uint64_t tok_str
                        const uint32_t *key_idx, uint8_t *pt, uint64_t pt_stride, uint32_t *pt_len,
                        int32_t *status, uint32_t n, void *stream);
 
+/* ---- irregular batches: length bucketing -------------------------------- */
+/* With RT_F_SORT_BY_LENGTH the batch is first grouped by length on the device
+ * (three small kernels on the same stream) so that the lanes of a wavefront
+ * carry packets of similar length; outputs stay at their own offsets, so the
+ * result is identical to rt_encrypt / rt_decrypt.  `workspace` is a DEVICE
+ * buffer of at least rt_workspace_bytes(n) bytes, owned by the caller and not
+ * reused until the call's work on `stream` has completed. */
+#define RT_F_SORT_BY_LENGTH 1u
+uint64_t rt_workspace_bytes(uint32_t n);
+int rt_encrypt_ex(const rt_keyset *ks, const uint8_t *pt, const uint64_t *pt_off, const uint32_t *pt_len,
+                  const uint32_t *key_idx, const uint8_t *iv, uint8_t *tok, const uint64_t *tok_off,
+                  uint32_t n, uint32_t flags, void *workspace, void *stream);
+int rt_decrypt_ex(const rt_keyset *ks, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,
+                  const uint32_t *key_idx, uint8_t *pt, const uint64_t *pt_off, uint32_t *pt_len,
+                  int32_t *status, uint32_t n, uint32_t flags, void *workspace, void *stream);
+
 /* ---- host-buffer convenience (PCIe-inclusive path) ----------------------- */
 /* Same meaning with HOST pointers; H2D, kernel, D2H on the context's stream,
  * synchronised before return. */

@@ -12,6 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "librnstok.so")
 
 RT_OK, RT_E_INVAL, RT_E_HIP, RT_E_NOMEM, RT_E_NODEV = 0, -1, -2, -3, -4
+RT_F_SORT_BY_LENGTH = 1
 RT_ST_OK, RT_ST_TOO_SHORT, RT_ST_BAD_HMAC, RT_ST_BAD_CT_LEN, RT_ST_BAD_PAD = 0, 1, 2, 3, 4
 
 # (name, restype, argtypes) for every entry point declared in include/rnstok.h
@@ -32,6 +33,9 @@ SIGNATURES = [
     ("rt_encrypt_uniform", _int, [_vp, _vp, _u64, _u32, _vp, _vp, _vp, _u64, _u32, _vp]),
     ("rt_decrypt", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),
     ("rt_decrypt_uniform", _int, [_vp, _vp, _u64, _u32, _vp, _vp, _u64, _vp, _vp, _u32, _vp]),
+    ("rt_workspace_bytes", _u64, [_u32]),
+    ("rt_encrypt_ex", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp]),
+    ("rt_decrypt_ex", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp]),
     ("rt_encrypt_host", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32]),
     ("rt_decrypt_host", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32]),
     ("rt_device_alloc", _vp, [_vp, _u64]),

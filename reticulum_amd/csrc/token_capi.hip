@@ -271,6 +271,46 @@ int rt_decrypt_uniform(const rt_keyset *k, const uint8_t *tok, uint64_t tok_stri
     return dec_common(k, a, stream);
 }
 
+uint64_t rt_workspace_bytes(uint32_t n) { return sort_workspace_bytes(n); }
+
+int rt_encrypt_ex(const rt_keyset *k, const uint8_t *pt, const uint64_t *pt_off, const uint32_t *pt_len,
+                  const uint32_t *key_idx, const uint8_t *iv, uint8_t *tok, const uint64_t *tok_off, uint32_t n,
+                  uint32_t flags, void *workspace, void *stream) {
+    if (n && (!pt_off || !pt_len || !tok_off)) return fail(RT_E_INVAL, "rt_encrypt_ex: null offset/length array");
+    if (flags & ~RT_F_SORT_BY_LENGTH) return fail(RT_E_INVAL, "rt_encrypt_ex: unknown flags");
+    int rc = check_keyset(k);
+    if (rc) return rc;
+    EncArgs a{};
+    a.pt = pt; a.pt_off = pt_off; a.pt_len = pt_len; a.key_idx = key_idx; a.iv = iv;
+    a.tok = tok; a.tok_off = tok_off; a.n = n;
+    if ((flags & RT_F_SORT_BY_LENGTH) && n > 1) {
+        if (!workspace) return fail(RT_E_INVAL, "rt_encrypt_ex: RT_F_SORT_BY_LENGTH needs a workspace");
+        RT_HIP(hipSetDevice(k->ctx->device), "hipSetDevice");
+        RT_HIP(launch_length_order(pt_len, n, 0, workspace, &a.order, k->ctx->n_cu, pick(k->ctx, stream)),
+               "length order");
+    }
+    return enc_common(k, a, stream);
+}
+
+int rt_decrypt_ex(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,
+                  const uint32_t *key_idx, uint8_t *pt, const uint64_t *pt_off, uint32_t *pt_len, int32_t *status,
+                  uint32_t n, uint32_t flags, void *workspace, void *stream) {
+    if (n && (!tok_off || !tok_len || !pt_off)) return fail(RT_E_INVAL, "rt_decrypt_ex: null offset/length array");
+    if (flags & ~RT_F_SORT_BY_LENGTH) return fail(RT_E_INVAL, "rt_decrypt_ex: unknown flags");
+    int rc = check_keyset(k);
+    if (rc) return rc;
+    DecArgs a{};
+    a.tok = tok; a.tok_off = tok_off; a.tok_len = tok_len; a.key_idx = key_idx; a.pt = pt; a.pt_off = pt_off;
+    a.out_len = pt_len; a.status = status; a.n = n;
+    if ((flags & RT_F_SORT_BY_LENGTH) && n > 1) {
+        if (!workspace) return fail(RT_E_INVAL, "rt_decrypt_ex: RT_F_SORT_BY_LENGTH needs a workspace");
+        RT_HIP(hipSetDevice(k->ctx->device), "hipSetDevice");
+        RT_HIP(launch_length_order(tok_len, n, 1, workspace, &a.order, k->ctx->n_cu, pick(k->ctx, stream)),
+               "length order");
+    }
+    return dec_common(k, a, stream);
+}
+
 // ---------------------------------------------------------------- host path
 
 static int ensure_work(rt_ctx *c, uint64_t bytes) {

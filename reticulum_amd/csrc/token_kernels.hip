@@ -155,7 +155,8 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
     const Layout in{a.pt_off, a.pt_stride, a.pt_len, a.uni_len};
     const uint32_t nthreads = gridDim.x * blockDim.x;
 
-    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < a.n; p += nthreads) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += nthreads) {
+        const uint32_t p = a.order ? a.order[i] : i;
         if (PERKEY) {
             const uint32_t *r = a.rec + (uint64_t)a.key_idx[p] * REC_WORDS;
             K.load(r, REC_ENC);
@@ -241,6 +242,140 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
     }
 }
 
+// ---------------------------------------------------- encrypt, long tokens --
+//
+// Few, long tokens (e.g. 16 KiB Resource segments sharded over 8 GPUs leave
+// 128 tokens per CU): one packet per lane no longer fills the machine, and
+// each lane's AES chain (latency-bound on LDS) and SHA chain (VALU) would run
+// back to back.  Here a workgroup of 2*G waves serves G groups of 64 tokens:
+// wave g (< G) runs the CBC chains of group g and drops each quad of
+// ciphertext into an LDS ring; wave G+g hashes the previous quad of the same
+// group.  One __syncthreads() per quad step keeps producer and consumer one
+// step apart (double-buffered ring after the 128 KiB table image).
+constexpr uint32_t RING_BASE = LDS_ENC_BYTES;                 // 0x20000
+constexpr uint32_t RING_BYTES = 2u * 2u * 64u * 64u;                           // G <= 2 groups x 2 slots
+constexpr uint32_t STEP_WORD = RING_BASE + RING_BYTES;                         // workgroup max of quad steps
+constexpr uint32_t LDS_ENC_LONG_BYTES = STEP_WORD + 16u;
+// (no static __shared__ here: the absolute LDS addresses assume the dynamic
+// region starts at 0)
+
+__device__ __forceinline__ void ring_put(uint32_t grp, uint32_t slot, uint32_t lane, const u32x4 c[4]) {
+    typedef __attribute__((address_space(3))) u32x4 l128;
+    l128 *r = (l128 *)(uintptr_t)(RING_BASE + ((grp * 2u + slot) * 64u + lane) * 64u);
+    r[0] = c[0]; r[1] = c[1]; r[2] = c[2]; r[3] = c[3];
+}
+__device__ __forceinline__ void ring_get(uint32_t grp, uint32_t slot, uint32_t lane, u32x4 c[4]) {
+    typedef __attribute__((address_space(3))) const u32x4 l128;
+    l128 *r = (l128 *)(uintptr_t)(RING_BASE + ((grp * 2u + slot) * 64u + lane) * 64u);
+    c[0] = r[0]; c[1] = r[1]; c[2] = r[2]; c[3] = r[3];
+}
+
+template <int NR, bool PERKEY>
+__global__ __launch_bounds__(256) void k_encrypt_long(EncArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
+    typedef __attribute__((address_space(3))) uint32_t lds_word;
+    lds_word *max_steps = (lds_word *)(uintptr_t)STEP_WORD;
+    fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);
+    const Lanes LN(threadIdx.x & 31u);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t G = blockDim.x >> 7;
+    const bool aes = wave < G;
+    const uint32_t grp = aes ? wave : wave - G;
+    const Layout in{a.pt_off, a.pt_stride, a.pt_len, a.uni_len};
+    Keys<NR, PERKEY> K;
+    if (!PERKEY && aes) K.load(a.rec, REC_ENC);
+
+    for (uint32_t base = blockIdx.x * G * 64u; base < a.n; base += gridDim.x * G * 64u) {
+        const uint32_t i = base + grp * 64u + lane;
+        const bool valid = i < a.n;
+        const uint32_t p = valid ? (a.order ? a.order[i] : i) : 0u;
+        const uint32_t L = valid ? in.l(p) : 0u;
+        const uint32_t nfull = L >> 4, nq = nfull >> 2, tb = (nfull & 3u) + 1u;
+        const uint32_t steps = valid ? nq + 1u : 0u;          // full quads + the tail quad
+        if (threadIdx.x == 0) *max_steps = 0;
+        __syncthreads();
+        __hip_atomic_fetch_max(max_steps, steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __syncthreads();
+        const uint32_t Q = *max_steps;
+        __syncthreads();          // everyone has read Q before the word is reset next iteration
+        const uint8_t *P = a.pt + (valid ? in.o(p) : 0);
+        uint8_t *O = a.tok + (valid ? (a.tok_off ? a.tok_off[p] : (uint64_t)p * a.tok_stride) : 0);
+        const uint32_t *rec = PERKEY && valid ? a.rec + (uint64_t)a.key_idx[p] * REC_WORDS : a.rec;
+        const u32x4 iv = valid ? ld16(a.iv + 16ull * p) : u32x4{0u, 0u, 0u, 0u};
+        if (aes) {
+            if (PERKEY && valid) K.load(rec, REC_ENC);
+            Sha256 dummy;
+            u32x4 prev = iv, x[4], c[4];
+            if (valid) st16(O, iv);
+            for (uint32_t k = 0; k < Q; ++k) {
+                if (k < steps) {
+                    const uint8_t *Pk = P + 64ull * k;
+                    if (k < nq) {
+                        x[0] = ld16(Pk); x[1] = ld16(Pk + 16); x[2] = ld16(Pk + 32); x[3] = ld16(Pk + 48);
+                    } else {
+                        const u32x4 z = {0u, 0u, 0u, 0u};
+                        const uint32_t r = L & 15u;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            x[j] = (uint32_t)j + 1u < tb ? ld16(Pk + 16 * j)
+                                                         : ((uint32_t)j + 1u == tb ? pad_block(Pk + 16 * j, r) : z);
+                    }
+                    enc_quad<NR, false>(c, x, prev, K.rk, LN, dummy);
+                    uint8_t *Ck = O + 16 + 64ull * k;
+                    const uint32_t nst = k < nq ? 4u : tb;
+                    st16(Ck, c[0]);
+                    if (nst > 1) st16(Ck + 16, c[1]);
+                    if (nst > 2) st16(Ck + 32, c[2]);
+                    if (nst > 3) st16(Ck + 48, c[3]);
+                    ring_put(grp, k & 1u, lane, c);
+                    prev = c[3];
+                }
+                __syncthreads();     // quad k visible to the SHA wave; SHA done with slot (k-1)&1
+            }
+            __syncthreads();         // matches the consumer's final step
+        } else {
+            uint32_t h[8], opad[8];
+            if (PERKEY) {
+                if (valid) { load8(h, rec + REC_IPAD); load8(opad, rec + REC_OPAD); }
+            } else {
+                load_uniform8(h, a.rec + REC_IPAD);
+                load_uniform8(opad, a.rec + REC_OPAD);
+            }
+            u32x4 prev = iv, c[4];
+            const uint64_t bits = (uint64_t)(64u + 16u + 16u * (nfull + 1u)) * 8u;
+            __syncthreads();         // step 0: nothing to hash yet
+            for (uint32_t k = 1; k <= Q; ++k) {
+                if (k <= steps) {
+                    ring_get(grp, (k - 1) & 1u, lane, c);
+                    if (k - 1 < nq) {
+                        uint32_t w[16];
+                        sha_units(w, prev, c[0], c[1], c[2]);
+                        sha256_compress(h, w);
+                        prev = c[3];
+                    } else {
+                        // tail quad: units prev, c[0..tb-1] (+ final padding), then the outer hash
+                        const uint32_t tu = tb + 1;
+                        if (tu >= 4) {
+                            uint32_t w[16];
+                            sha_units(w, prev, c[0], c[1], c[2]);
+                            sha256_compress(h, w);
+                            sha_final_units(h, tu - 4, c[3], c[3], c[3], bits);
+                        } else {
+                            sha_final_units(h, tu, prev, c[0], c[1], bits);
+                        }
+                        uint32_t tag[8];
+                        hmac_outer(tag, h, opad);
+                        uint8_t *T = O + 16 + 16ull * (nfull + 1u);
+                        st16(T, u32x4{bswap(tag[0]), bswap(tag[1]), bswap(tag[2]), bswap(tag[3])});
+                        st16(T + 16, u32x4{bswap(tag[4]), bswap(tag[5]), bswap(tag[6]), bswap(tag[7])});
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    }
+}
+
 // --------------------------------------------------------------- decrypt --
 
 template <int NR, bool PERKEY>
@@ -258,7 +393,8 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_DEC : WG_DEC) void k_decr
     const Layout in{a.tok_off, a.tok_stride, a.tok_len, a.uni_len};
     const uint32_t nthreads = gridDim.x * blockDim.x;
 
-    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < a.n; p += nthreads) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += nthreads) {
+        const uint32_t p = a.order ? a.order[i] : i;
         const uint32_t *r = a.rec;
         if (PERKEY) {
             r = a.rec + (uint64_t)a.key_idx[p] * REC_WORDS;
@@ -359,6 +495,87 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_DEC : WG_DEC) void k_decr
         a.status[p] = st;
         a.out_len[p] = outlen;
     }
+}
+
+// ------------------------------------------------------ length bucketing --
+//
+// Three small passes (histogram, scan, scatter) build a permutation that
+// groups packets by descending quad count (64-B steps of the CBC/SHA loop).
+// Per-workgroup LDS histograms keep global atomics to one per (workgroup,
+// bucket).  Within a bucket the order is arbitrary.
+
+__device__ __forceinline__ uint32_t sort_bucket(uint32_t len, int dec) {
+    const uint32_t body = dec ? (len > 48u ? len - 48u : 0u) : len;
+    const uint32_t q = body >> 6;
+    return SORT_BUCKETS - 1u - (q < SORT_BUCKETS - 1u ? q : SORT_BUCKETS - 1u);   // descending
+}
+
+constexpr uint32_t SORT_TILE = 8192;   // packets per workgroup in the scatter pass
+
+__global__ __launch_bounds__(1024) void k_sort_hist(const uint32_t *len, uint32_t n, int dec, uint32_t *hist) {
+    __shared__ uint32_t h[SORT_BUCKETS];
+    for (uint32_t b = threadIdx.x; b < SORT_BUCKETS; b += blockDim.x) h[b] = 0;
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        atomicAdd(&h[sort_bucket(len[i], dec)], 1u);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < SORT_BUCKETS; b += blockDim.x)
+        if (h[b]) atomicAdd(&hist[b], h[b]);
+}
+
+__global__ __launch_bounds__(1024) void k_sort_scan(uint32_t *hist) {
+    // exclusive scan of SORT_BUCKETS counters in place (one workgroup)
+    __shared__ uint32_t part[1024];
+    constexpr uint32_t PER = SORT_BUCKETS / 1024;
+    uint32_t v[PER], sum = 0;
+    for (uint32_t k = 0; k < PER; ++k) { v[k] = hist[threadIdx.x * PER + k]; sum += v[k]; }
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint32_t t = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += t;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - sum;
+    for (uint32_t k = 0; k < PER; ++k) { hist[threadIdx.x * PER + k] = run; run += v[k]; }
+}
+
+__global__ __launch_bounds__(1024) void k_sort_scatter(const uint32_t *len, uint32_t n, int dec, uint32_t *cursor,
+                                                       uint32_t *order) {
+    __shared__ uint32_t cnt[SORT_BUCKETS];
+    __shared__ uint32_t base[SORT_BUCKETS];
+    const uint32_t lo = blockIdx.x * SORT_TILE, hi = lo + SORT_TILE < n ? lo + SORT_TILE : n;
+    for (uint32_t b = threadIdx.x; b < SORT_BUCKETS; b += blockDim.x) cnt[b] = 0;
+    __syncthreads();
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&cnt[sort_bucket(len[i], dec)], 1u);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < SORT_BUCKETS; b += blockDim.x) {
+        base[b] = cnt[b] ? atomicAdd(&cursor[b], cnt[b]) : 0u;
+        cnt[b] = 0;
+    }
+    __syncthreads();
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        const uint32_t b = sort_bucket(len[i], dec);
+        order[base[b] + atomicAdd(&cnt[b], 1u)] = i;
+    }
+}
+
+uint64_t sort_workspace_bytes(uint32_t n) { return ((uint64_t)n * 4 + 255) / 256 * 256 + 2ull * SORT_BUCKETS * 4; }
+
+hipError_t launch_length_order(const uint32_t *len, uint32_t n, int dec, void *workspace, const uint32_t **order,
+                               int n_cu, hipStream_t s) {
+    uint32_t *ord = (uint32_t *)workspace;
+    uint32_t *hist = (uint32_t *)((uint8_t *)workspace + ((uint64_t)n * 4 + 255) / 256 * 256);
+    hipError_t e = hipMemsetAsync(hist, 0, SORT_BUCKETS * 4, s);
+    if (e != hipSuccess) return e;
+    const int gh = n_cu < (int)((n + 1023) / 1024) ? n_cu : (int)((n + 1023) / 1024);
+    hipLaunchKernelGGL(k_sort_hist, dim3(gh > 0 ? gh : 1), dim3(1024), 0, s, len, n, dec, hist);
+    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(1024), 0, s, hist);
+    hipLaunchKernelGGL(k_sort_scatter, dim3((n + SORT_TILE - 1) / SORT_TILE), dim3(1024), 0, s, len, n, dec, hist,
+                       ord);
+    *order = ord;
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------- key setup --
@@ -466,7 +683,27 @@ static hipError_t launch_dec_nr(const DecArgs &a, Shape sh, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <int NR>
+static hipError_t launch_enc_long_nr(const EncArgs &a, int n_cu, hipStream_t s) {
+    const uint32_t G = a.n > 64u * (uint32_t)n_cu ? 2u : 1u;          // token groups of 64 per workgroup
+    uint64_t grid = (a.n + 64ull * G - 1) / (64ull * G);
+    if (grid > (uint64_t)n_cu) grid = n_cu;
+    if (a.key_idx)
+        hipLaunchKernelGGL((k_encrypt_long<NR, true>), dim3((unsigned)grid), dim3(128 * G), LDS_ENC_LONG_BYTES, s, a);
+    else
+        hipLaunchKernelGGL((k_encrypt_long<NR, false>), dim3((unsigned)grid), dim3(128 * G), LDS_ENC_LONG_BYTES, s, a);
+    return hipGetLastError();
+}
+
+// Long-token mode: uniform batches of >= 1 KiB packets that give each CU at
+// most two waves of packets in the one-lane-per-packet kernel.
+static bool use_long(uint32_t n, const uint32_t *len, uint32_t uni, int n_cu) {
+    return len == nullptr && uni >= 1024u && (uint64_t)n <= 128ull * (uint64_t)n_cu;
+}
+
 hipError_t launch_encrypt(const EncArgs &a, int nr, int n_cu, hipStream_t s) {
+    if (use_long(a.n, a.pt_len, a.uni_len, n_cu))
+        return nr == 14 ? launch_enc_long_nr<14>(a, n_cu, s) : launch_enc_long_nr<10>(a, n_cu, s);
     const Shape sh = shape_for(a.n, a.key_idx ? WG_PERKEY_ENC : WG_ENC, n_cu);
     return nr == 14 ? launch_enc_nr<14>(a, sh, s) : launch_enc_nr<10>(a, sh, s);
 }
@@ -489,6 +726,10 @@ hipError_t configure_kernels() {
     RT_CFG((k_encrypt<14, true>), LDS_ENC_BYTES);
     RT_CFG((k_encrypt<10, false>), LDS_ENC_BYTES);
     RT_CFG((k_encrypt<10, true>), LDS_ENC_BYTES);
+    RT_CFG((k_encrypt_long<14, false>), LDS_ENC_LONG_BYTES);
+    RT_CFG((k_encrypt_long<14, true>), LDS_ENC_LONG_BYTES);
+    RT_CFG((k_encrypt_long<10, false>), LDS_ENC_LONG_BYTES);
+    RT_CFG((k_encrypt_long<10, true>), LDS_ENC_LONG_BYTES);
     RT_CFG((k_decrypt<14, false>), LDS_DEC_BYTES);
     RT_CFG((k_decrypt<14, true>), LDS_DEC_BYTES);
     RT_CFG((k_decrypt<10, false>), LDS_DEC_BYTES);

@@ -18,6 +18,7 @@ struct EncArgs {
     uint8_t *tok;
     const uint64_t *tok_off;    // null -> i * tok_stride
     uint64_t tok_stride;
+    const uint32_t *order;      // null -> lane i handles packet i; else packet order[i]
     uint32_t n;
 };
 
@@ -35,10 +36,19 @@ struct DecArgs {
     uint64_t pt_stride;
     uint32_t *out_len;
     int32_t *status;
+    const uint32_t *order;      // null -> lane i handles token i; else token order[i]
     uint32_t n;
 };
 
 hipError_t configure_kernels();
+
+// Length bucketing: order[] = packet indices grouped by descending AES quad
+// count, so that the lanes of a wave carry similar lengths.  `dec` selects
+// token lengths (quads of the ciphertext body) instead of plaintext lengths.
+constexpr uint32_t SORT_BUCKETS = 4096;
+uint64_t sort_workspace_bytes(uint32_t n);    // order[n] + 2 x SORT_BUCKETS counters
+hipError_t launch_length_order(const uint32_t *len, uint32_t n, int dec, void *workspace, const uint32_t **order,
+                               int n_cu, hipStream_t s);
 hipError_t launch_encrypt(const EncArgs &a, int nr, int n_cu, hipStream_t s);
 hipError_t launch_decrypt(const DecArgs &a, int nr, int n_cu, hipStream_t s);
 hipError_t launch_key_setup(const uint8_t *keys, uint32_t key_len, uint32_t n_keys, const uint8_t *sbox,

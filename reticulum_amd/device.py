@@ -58,19 +58,38 @@ def decrypt_uniform(ks: KeySet, tok, tok_len, pt, out_len, status, key_idx=None,
                                          pt.stride(0), _p(out_len), _p(status), n, _stream(stream)))
 
 
-def encrypt(ks: KeySet, pt, pt_off, pt_len, iv, tok, tok_off, key_idx=None, stream=None):
+def _workspace(n, device):
+    lib = _native.load()
+    return torch.empty(int(lib.rt_workspace_bytes(n)), dtype=torch.uint8, device=device)
+
+
+def encrypt(ks: KeySet, pt, pt_off, pt_len, iv, tok, tok_off, key_idx=None, stream=None, sort=False,
+            workspace=None):
     """Variable-length batch: pt/tok flat uint8 buffers, pt_off/tok_off int64,
-    pt_len int32, iv (n,16) uint8."""
+    pt_len int32, iv (n,16) uint8.  ``sort=True`` groups packets by length on
+    the device first (same outputs; wavefronts carry similar lengths)."""
     _check_u8(pt, iv, tok)
     n = pt_off.numel()
     lib = _native.load()
+    if sort:
+        ws = workspace if workspace is not None else _workspace(n, pt.device)
+        _native.check(lib.rt_encrypt_ex(ks.handle, _p(pt), _p(pt_off), _p(pt_len), _p(key_idx), _p(iv), _p(tok),
+                                        _p(tok_off), n, _native.RT_F_SORT_BY_LENGTH, _p(ws), _stream(stream)))
+        return
     _native.check(lib.rt_encrypt(ks.handle, _p(pt), _p(pt_off), _p(pt_len), _p(key_idx), _p(iv), _p(tok),
                                  _p(tok_off), n, _stream(stream)))
 
 
-def decrypt(ks: KeySet, tok, tok_off, tok_len, pt, pt_off, out_len, status, key_idx=None, stream=None):
+def decrypt(ks: KeySet, tok, tok_off, tok_len, pt, pt_off, out_len, status, key_idx=None, stream=None, sort=False,
+            workspace=None):
     _check_u8(tok, pt)
     n = tok_off.numel()
     lib = _native.load()
+    if sort:
+        ws = workspace if workspace is not None else _workspace(n, tok.device)
+        _native.check(lib.rt_decrypt_ex(ks.handle, _p(tok), _p(tok_off), _p(tok_len), _p(key_idx), _p(pt),
+                                        _p(pt_off), _p(out_len), _p(status), n, _native.RT_F_SORT_BY_LENGTH, _p(ws),
+                                        _stream(stream)))
+        return
     _native.check(lib.rt_decrypt(ks.handle, _p(tok), _p(tok_off), _p(tok_len), _p(key_idx), _p(pt), _p(pt_off),
                                  _p(out_len), _p(status), n, _stream(stream)))

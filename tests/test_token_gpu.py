@@ -230,3 +230,78 @@ def test_resource_chunks_16k(rt):
     ref, _, _ = _oracle_tokens(key.reshape(1, 64), pt_h[sel].reshape(-1), np.arange(len(sel), dtype=np.uint64) * L,
                                np.full(len(sel), L, np.uint32), iv_h[sel], None)
     assert np.array_equal(ref.reshape(len(sel), tl), tok.cpu().numpy()[sel])
+
+
+def test_sorted_variable_batch_matches_unsorted_and_oracle(rt):
+    """Config c5 shape (64..4096 B, many keys) through the length-bucketed
+    entry points: identical tokens to the unsorted launch and to the oracle,
+    and sorted decrypt restores every plaintext."""
+    import torch
+    from reticulum_amd import device
+    rng = np.random.Generator(np.random.PCG64(55))
+    n, nk = 20000, 4096
+    lens = rng.integers(64, 4097, n).astype(np.int32)
+    lens[:100] = rng.integers(0, 64, 100)              # and some short ones
+    keys = rng.integers(0, 256, (nk, 64), dtype=np.uint8)
+    kidx = rng.integers(0, nk, n).astype(np.int32)
+    off = np.zeros(n, np.int64)
+    off[1:] = np.cumsum(lens[:-1])
+    buf = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    ivs = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    tl = (16 + 16 * (lens // 16 + 1) + 32).astype(np.int32)
+    toff = np.zeros(n, np.int64)
+    toff[1:] = np.cumsum(tl[:-1])
+    ks = rt.KeySet(keys)
+    cu = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    d_pt, d_off, d_len, d_iv, d_k, d_toff, d_tl = cu(buf), cu(off), cu(lens), cu(ivs), cu(kidx), cu(toff), cu(tl)
+    tok_a = torch.zeros(int(tl.sum()), dtype=torch.uint8, device="cuda")
+    tok_b = torch.zeros_like(tok_a)
+    device.encrypt(ks, d_pt, d_off, d_len, d_iv, tok_a, d_toff, key_idx=d_k)
+    device.encrypt(ks, d_pt, d_off, d_len, d_iv, tok_b, d_toff, key_idx=d_k, sort=True)
+    torch.cuda.synchronize()
+    assert torch.equal(tok_a, tok_b)
+    ref, _, _ = _oracle_tokens(keys, buf, off.astype(np.uint64), lens.astype(np.uint32), ivs, kidx.astype(np.uint32))
+    assert np.array_equal(ref[:tok_a.numel()], tok_a.cpu().numpy())
+    # decrypt writes each token's whole body (tok_len - 48 bytes, pad block
+    # included) at its pt_off, so output regions are sized by capacity
+    cap = tl - 48
+    coff = np.zeros(n, np.int64)
+    coff[1:] = np.cumsum(cap[:-1])
+    back = torch.zeros(int(cap.sum()), dtype=torch.uint8, device="cuda")
+    ol = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    device.decrypt(ks, tok_b, d_toff, d_tl, back, cu(coff), ol, st, key_idx=d_k, sort=True)
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0
+    assert torch.equal(ol.cpu(), torch.from_numpy(lens))
+    bh = back.cpu().numpy()
+    for i in range(0, n, 37):
+        assert bh[coff[i]:coff[i] + lens[i]].tobytes() == buf[off[i]:off[i] + lens[i]].tobytes()
+
+
+@pytest.mark.parametrize("n,L", [(300, 1024), (300, 1500), (20000, 4095), (2048, 16391)])
+def test_long_token_mode_vs_oracle(rt, n, L):
+    """Uniform batches of long tokens with few packets per CU take the
+    producer/consumer kernel (AES wave -> LDS ring -> SHA wave); bit-exact vs
+    the oracle for every tail shape, and decrypt round-trips."""
+    import torch
+    from reticulum_amd import device
+    rng = np.random.Generator(np.random.PCG64(L))
+    tl = rt.token_len(L)
+    pt_h = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    iv_h = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    key = rng.integers(0, 256, 64, dtype=np.uint8)
+    ks = rt.KeySet(key.tobytes())
+    pt = torch.from_numpy(pt_h).cuda()
+    tok = torch.empty((n, tl), dtype=torch.uint8, device="cuda")
+    device.encrypt_uniform(ks, pt, L, torch.from_numpy(iv_h).cuda(), tok)
+    sel = np.unique(np.concatenate([np.arange(0, n, max(1, n // 40)), [n - 1]]))
+    ref, _, _ = _oracle_tokens(key.reshape(1, 64), pt_h[sel].reshape(-1), np.arange(len(sel), dtype=np.uint64) * L,
+                               np.full(len(sel), L, np.uint32), iv_h[sel], None)
+    assert np.array_equal(ref.reshape(len(sel), tl), tok.cpu().numpy()[sel])
+    back = torch.empty((n, tl - 48), dtype=torch.uint8, device="cuda")
+    ol = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    device.decrypt_uniform(ks, tok, tl, back, ol, st)
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0 and torch.equal(back[:, :L], pt)

@@ -94,6 +94,10 @@ struct Layout {
     __device__ __forceinline__ uint32_t l(uint32_t i) const { return len ? len[i] : uni; }
 };
 
+__device__ __forceinline__ uint64_t in_off(const uint64_t *off, uint64_t stride, uint32_t i) {
+    return off ? off[i] : (uint64_t)i * stride;
+}
+
 template <int NR, bool PERKEY>
 struct Keys {
     uint32_t rk[4 * (NR + 1)];
@@ -468,7 +472,7 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_DEC : WG_DEC) void k_decr
             if (tb > 2) st16(D + 32, pp[2]);
             if (tb > 3) st16(D + 48, pp[3]);
             const u32x4 last = tb == 1 ? pp[0] : (tb == 2 ? pp[1] : (tb == 3 ? pp[2] : pp[3]));
-            const u32x4 u0 = prev, u1 = c[0], u2 = c[1], u3 = c[2], u4 = c[3];
+            const u32x4 u0 = prev, u1 = c[0], u2 = c[1], u4 = c[3];
             const uint32_t tu = tb + 1;
             const uint64_t bits = (uint64_t)(64u + 16u + 16u * nb) * 8u;
             if (full)
@@ -494,6 +498,105 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_DEC : WG_DEC) void k_decr
         }
         a.status[p] = st;
         a.out_len[p] = outlen;
+    }
+}
+
+// ---------------------------------------------------- decrypt, long tokens --
+//
+// Few, long tokens, one key, uniform length T (48 + 16*nb, nb >= 61): CBC
+// decryption is block-parallel, only the HMAC is a serial chain.  A 512-thread
+// workgroup serves 128 tokens: waves 0-1 run the HMAC chains (one token per
+// lane, reading the ciphertext straight from HBM), waves 2-7 decrypt the
+// tokens' quads as independent work items (4 blocks each).  After a barrier
+// the HMAC lanes read their token's last plaintext byte, set the status and
+// zero the region of any token that failed.
+template <int NR>
+__global__ __launch_bounds__(512) void k_decrypt_long(DecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
+    fill_tables<true>(tab_u32, a.sbox, a.sbox + 256);
+    const Lanes LN(threadIdx.x & 31u);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    constexpr uint32_t TOK = 128, SHA_WAVES = 2;
+    const uint32_t T = a.uni_len, nb = (T - 48u) >> 4, nquads = (nb + 3u) >> 2, tbl = nb - 4u * (nquads - 1u);
+    const bool sha = wave < SHA_WAVES;
+#ifdef RNSTOK_DEC_LONG_PRIO
+    if (sha) __builtin_amdgcn_s_setprio(RNSTOK_DEC_LONG_PRIO);
+#endif
+    Keys<NR, false> K;
+    if (!sha) K.load(a.rec, REC_DEC);
+    const uint32_t aes_lanes = blockDim.x - SHA_WAVES * 64u, aes_id = threadIdx.x - SHA_WAVES * 64u;
+
+    for (uint32_t base = blockIdx.x * TOK; base < a.n; base += gridDim.x * TOK) {
+        const uint32_t ntok = a.n - base < TOK ? a.n - base : TOK;
+        uint32_t diff = 1;
+        if (sha) {
+            const uint32_t t = base + wave * 64u + lane;
+            if (t < a.n) {
+                const uint32_t p = a.order ? a.order[t] : t;
+                const uint8_t *Kt = a.tok + in_off(a.tok_off, a.tok_stride, p);
+                uint32_t h[8], opad[8];
+                load_uniform8(h, a.rec + REC_IPAD);
+                load_uniform8(opad, a.rec + REC_OPAD);
+                const uint32_t M = T - 32u, full = M >> 6;
+                for (uint32_t i = 0; i < full; ++i) {
+                    uint32_t w[16];
+                    const uint8_t *B = Kt + 64ull * i;
+                    sha_units(w, ld16(B), ld16(B + 16), ld16(B + 32), ld16(B + 48));
+                    sha256_compress(h, w);
+                }
+                const uint32_t fu = (M - 64u * full) >> 4;
+                const u32x4 z = {0u, 0u, 0u, 0u};
+                const uint8_t *R = Kt + 64ull * full;
+                sha_final_units(h, fu, fu > 0 ? ld16(R) : z, fu > 1 ? ld16(R + 16) : z, fu > 2 ? ld16(R + 32) : z,
+                                (uint64_t)(64u + M) * 8u);
+                uint32_t tag[8];
+                hmac_outer(tag, h, opad);
+                const u32x4 r0 = ld16(Kt + M), r1 = ld16(Kt + M + 16);
+                diff = (r0.x ^ bswap(tag[0])) | (r0.y ^ bswap(tag[1])) | (r0.z ^ bswap(tag[2])) |
+                       (r0.w ^ bswap(tag[3])) | (r1.x ^ bswap(tag[4])) | (r1.y ^ bswap(tag[5])) |
+                       (r1.z ^ bswap(tag[6])) | (r1.w ^ bswap(tag[7]));
+            }
+        } else {
+            Sha256 dummy;
+            const uint32_t items = ntok * nquads;
+            for (uint32_t j = aes_id; j < items; j += aes_lanes) {
+                const uint32_t t = base + j % ntok, q = j / ntok;
+                const uint32_t p = a.order ? a.order[t] : t;
+                const uint8_t *C = a.tok + in_off(a.tok_off, a.tok_stride, p) + 16 + 64ull * q;
+                uint8_t *D = a.pt + in_off(a.pt_off, a.pt_stride, p) + 64ull * q;
+                const uint32_t nbk = q + 1u == nquads ? tbl : 4u;
+                const u32x4 z = {0u, 0u, 0u, 0u};
+                u32x4 c[4], pp[4];
+                c[0] = ld16(C);
+                c[1] = nbk > 1 ? ld16(C + 16) : z;
+                c[2] = nbk > 2 ? ld16(C + 32) : z;
+                c[3] = nbk > 3 ? ld16(C + 48) : z;
+                const u32x4 chain = ld16(C - 16);      // previous ciphertext block (the IV for q = 0)
+                dec_quad<NR, false>(pp, c, chain, K.rk, LN, dummy);
+                st16(D, pp[0]);
+                if (nbk > 1) st16(D + 16, pp[1]);
+                if (nbk > 2) st16(D + 32, pp[2]);
+                if (nbk > 3) st16(D + 48, pp[3]);
+            }
+        }
+        __syncthreads();          // plaintext of every token of this block is written
+        if (sha) {
+            const uint32_t t = base + wave * 64u + lane;
+            if (t < a.n) {
+                const uint32_t p = a.order ? a.order[t] : t;
+                uint8_t *O = a.pt + in_off(a.pt_off, a.pt_stride, p);
+                const uint32_t padn = O[16u * nb - 1u];       // PKCS7.unpad: n = data[-1]
+                const int32_t st = diff ? 2 : (padn > 16u ? 4 : 0);
+                uint32_t outlen = st == 0 ? 16u * nb - padn : (st == 4 ? padn : 0u);
+                if (st != 0) {
+                    const u32x4 z = {0u, 0u, 0u, 0u};
+                    for (uint32_t i = 0; i < nb; ++i) st16(O + 16 * i, z);
+                }
+                a.status[p] = st;
+                a.out_len[p] = outlen;
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -707,7 +810,23 @@ hipError_t launch_encrypt(const EncArgs &a, int nr, int n_cu, hipStream_t s) {
     const Shape sh = shape_for(a.n, a.key_idx ? WG_PERKEY_ENC : WG_ENC, n_cu);
     return nr == 14 ? launch_enc_nr<14>(a, sh, s) : launch_enc_nr<10>(a, sh, s);
 }
+#ifndef RNSTOK_DEC_LONG_WAVES
+#define RNSTOK_DEC_LONG_WAVES 8
+#endif
+template <int NR>
+static hipError_t launch_dec_long_nr(const DecArgs &a, int n_cu, hipStream_t s) {
+    uint64_t grid = (a.n + 127ull) / 128ull;
+    if (grid > (uint64_t)n_cu) grid = n_cu;
+    hipLaunchKernelGGL((k_decrypt_long<NR>), dim3((unsigned)grid), dim3(64 * RNSTOK_DEC_LONG_WAVES), LDS_DEC_BYTES, s,
+                       a);
+    return hipGetLastError();
+}
+
 hipError_t launch_decrypt(const DecArgs &a, int nr, int n_cu, hipStream_t s) {
+    // long mode: one key, uniform well-formed tokens of >= 1 KiB body, few per CU
+    if (!a.key_idx && a.tok_len == nullptr && a.uni_len >= 48u + 1024u && ((a.uni_len - 48u) & 15u) == 0 &&
+        (uint64_t)a.n <= 128ull * (uint64_t)n_cu)
+        return nr == 14 ? launch_dec_long_nr<14>(a, n_cu, s) : launch_dec_long_nr<10>(a, n_cu, s);
     const Shape sh = shape_for(a.n, a.key_idx ? WG_PERKEY_DEC : WG_DEC, n_cu);
     return nr == 14 ? launch_dec_nr<14>(a, sh, s) : launch_dec_nr<10>(a, sh, s);
 }
@@ -726,6 +845,8 @@ hipError_t configure_kernels() {
     RT_CFG((k_encrypt<14, true>), LDS_ENC_BYTES);
     RT_CFG((k_encrypt<10, false>), LDS_ENC_BYTES);
     RT_CFG((k_encrypt<10, true>), LDS_ENC_BYTES);
+    RT_CFG((k_decrypt_long<14>), LDS_DEC_BYTES);
+    RT_CFG((k_decrypt_long<10>), LDS_DEC_BYTES);
     RT_CFG((k_encrypt_long<14, false>), LDS_ENC_LONG_BYTES);
     RT_CFG((k_encrypt_long<14, true>), LDS_ENC_LONG_BYTES);
     RT_CFG((k_encrypt_long<10, false>), LDS_ENC_LONG_BYTES);

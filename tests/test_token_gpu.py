@@ -305,3 +305,61 @@ def test_long_token_mode_vs_oracle(rt, n, L):
     device.decrypt_uniform(ks, tok, tl, back, ol, st)
     torch.cuda.synchronize()
     assert int(st.abs().sum()) == 0 and torch.equal(back[:, :L], pt)
+
+
+@pytest.mark.parametrize("klen", [64, 32])
+def test_long_decrypt_statuses(rt, klen):
+    """Long-token decrypt (block-parallel AES + serial HMAC lanes): tokens with
+    valid HMAC but a bad / zero / short pad byte, and tampered tokens, give the
+    reference statuses (Token.py:103-114, PKCS7.unpad) and the same outputs as
+    the general kernel (variable-length entry, no long mode)."""
+    import hashlib
+    import hmac as hm
+    import torch
+    from reticulum_amd import device
+    rng = np.random.Generator(np.random.PCG64(77 + klen))
+    n, m = 300, 65                            # body = 16*m bytes >= 1 KiB
+    key = rng.integers(0, 256, klen, dtype=np.uint8)
+    ks = rt.KeySet(key.tobytes())
+    x = rng.integers(0, 256, (n, 16 * m), dtype=np.uint8)
+    x[:, -1] = np.array([0x20, 0x05, 0x00, 0x10, 0x11], np.uint8)[np.arange(n) % 5]
+    iv = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    full = torch.empty((n, rt.token_len(16 * m)), dtype=torch.uint8, device="cuda")
+    device.encrypt_uniform(ks, torch.from_numpy(x).cuda(), 16 * m, torch.from_numpy(iv).cuda(), full)
+    fh = full.cpu().numpy()
+    sk = key[: klen // 2].tobytes()
+    tl = 16 + 16 * m + 32
+    toks = np.zeros((n, tl), np.uint8)
+    for i in range(n):                       # drop the all-pad block, re-MAC: last byte of x is the pad byte
+        body = fh[i, : 16 + 16 * m].tobytes()
+        toks[i] = np.frombuffer(body + hm.new(sk, body, hashlib.sha256).digest(), np.uint8)
+    toks[7::11, 100] ^= 1                     # tampered ciphertext
+    toks[9::13, -1] ^= 0x80                   # tampered tag
+    tok = torch.from_numpy(toks).cuda()
+
+    def run(uniform):
+        back = torch.full((n, 16 * m), 0xAA, dtype=torch.uint8, device="cuda")
+        ol = torch.empty(n, dtype=torch.int32, device="cuda")
+        st = torch.empty(n, dtype=torch.int32, device="cuda")
+        if uniform:
+            device.decrypt_uniform(ks, tok, tl, back, ol, st)
+        else:
+            offs = torch.arange(n, dtype=torch.int64, device="cuda")
+            lens = torch.full((n,), tl, dtype=torch.int32, device="cuda")
+            device.decrypt(ks, tok.reshape(-1), offs * tl, lens, back.reshape(-1), offs * (16 * m), ol, st)
+        torch.cuda.synchronize()
+        return back.cpu().numpy(), ol.cpu().numpy(), st.cpu().numpy()
+
+    b_long, ol_long, st_long = run(True)
+    b_gen, ol_gen, st_gen = run(False)
+    assert np.array_equal(st_long, st_gen) and np.array_equal(ol_long, ol_gen) and np.array_equal(b_long, b_gen)
+    for i in range(n):
+        tampered = (i >= 7 and (i - 7) % 11 == 0) or (i >= 9 and (i - 9) % 13 == 0)
+        padn = int(x[i, -1])
+        if tampered:
+            assert st_long[i] == 2 and ol_long[i] == 0 and not b_long[i].any(), i
+        elif padn > 16:
+            assert st_long[i] == 4 and ol_long[i] == padn and not b_long[i].any(), i
+        else:
+            assert st_long[i] == 0 and ol_long[i] == 16 * m - padn, i
+            assert np.array_equal(b_long[i, : 16 * m - padn], x[i, : 16 * m - padn]), i

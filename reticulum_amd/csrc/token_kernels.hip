@@ -309,13 +309,18 @@ __global__ __launch_bounds__(256) void k_encrypt_long(EncArgs a) {
         if (aes) {
             if (PERKEY && valid) K.load(rec, REC_ENC);
             Sha256 dummy;
-            u32x4 prev = iv, x[4], c[4];
+            u32x4 prev = iv, x[4], c[4], xn[4];
             if (valid) st16(O, iv);
+            if (nq > 0) { xn[0] = ld16(P); xn[1] = ld16(P + 16); xn[2] = ld16(P + 32); xn[3] = ld16(P + 48); }
             for (uint32_t k = 0; k < Q; ++k) {
                 if (k < steps) {
                     const uint8_t *Pk = P + 64ull * k;
                     if (k < nq) {
-                        x[0] = ld16(Pk); x[1] = ld16(Pk + 16); x[2] = ld16(Pk + 32); x[3] = ld16(Pk + 48);
+                        // the next quad's plaintext is requested before this quad's rounds (HBM latency hidden)
+                        x[0] = xn[0]; x[1] = xn[1]; x[2] = xn[2]; x[3] = xn[3];
+                        if (k + 1 < nq) {
+                            xn[0] = ld16(Pk + 64); xn[1] = ld16(Pk + 80); xn[2] = ld16(Pk + 96); xn[3] = ld16(Pk + 112);
+                        }
                     } else {
                         const u32x4 z = {0u, 0u, 0u, 0u};
                         const uint32_t r = L & 15u;
@@ -511,12 +516,15 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_DEC : WG_DEC) void k_decr
 // the HMAC lanes read their token's last plaintext byte, set the status and
 // zero the region of any token that failed.
 template <int NR>
-__global__ __launch_bounds__(512) void k_decrypt_long(DecArgs a) {
+__global__ __launch_bounds__(1024) void k_decrypt_long(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
     fill_tables<true>(tab_u32, a.sbox, a.sbox + 256);
     const Lanes LN(threadIdx.x & 31u);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    constexpr uint32_t TOK = 128, SHA_WAVES = 2;
+#ifndef RNSTOK_DEC_LONG_SHA_LANES
+#define RNSTOK_DEC_LONG_SHA_LANES 64
+#endif
+    constexpr uint32_t TOK = 128, SHA_LANES = RNSTOK_DEC_LONG_SHA_LANES, SHA_WAVES = TOK / SHA_LANES;
     const uint32_t T = a.uni_len, nb = (T - 48u) >> 4, nquads = (nb + 3u) >> 2, tbl = nb - 4u * (nquads - 1u);
     const bool sha = wave < SHA_WAVES;
 #ifdef RNSTOK_DEC_LONG_PRIO
@@ -530,18 +538,22 @@ __global__ __launch_bounds__(512) void k_decrypt_long(DecArgs a) {
         const uint32_t ntok = a.n - base < TOK ? a.n - base : TOK;
         uint32_t diff = 1;
         if (sha) {
-            const uint32_t t = base + wave * 64u + lane;
-            if (t < a.n) {
+            const uint32_t t = base + wave * SHA_LANES + lane;
+            if (lane < SHA_LANES && t < a.n) {
                 const uint32_t p = a.order ? a.order[t] : t;
                 const uint8_t *Kt = a.tok + in_off(a.tok_off, a.tok_stride, p);
                 uint32_t h[8], opad[8];
                 load_uniform8(h, a.rec + REC_IPAD);
                 load_uniform8(opad, a.rec + REC_OPAD);
-                const uint32_t M = T - 32u, full = M >> 6;
+                const uint32_t M = T - 32u, full = M >> 6;       // full >= 16 here
+                u32x4 b0 = ld16(Kt), b1 = ld16(Kt + 16), b2 = ld16(Kt + 32), b3 = ld16(Kt + 48);
                 for (uint32_t i = 0; i < full; ++i) {
                     uint32_t w[16];
-                    const uint8_t *B = Kt + 64ull * i;
-                    sha_units(w, ld16(B), ld16(B + 16), ld16(B + 32), ld16(B + 48));
+                    sha_units(w, b0, b1, b2, b3);
+                    if (i + 1 < full) {          // next block requested before this compression
+                        const uint8_t *B = Kt + 64ull * (i + 1);
+                        b0 = ld16(B); b1 = ld16(B + 16); b2 = ld16(B + 32); b3 = ld16(B + 48);
+                    }
                     sha256_compress(h, w);
                 }
                 const uint32_t fu = (M - 64u * full) >> 4;
@@ -581,8 +593,8 @@ __global__ __launch_bounds__(512) void k_decrypt_long(DecArgs a) {
         }
         __syncthreads();          // plaintext of every token of this block is written
         if (sha) {
-            const uint32_t t = base + wave * 64u + lane;
-            if (t < a.n) {
+            const uint32_t t = base + wave * SHA_LANES + lane;
+            if (lane < SHA_LANES && t < a.n) {
                 const uint32_t p = a.order ? a.order[t] : t;
                 uint8_t *O = a.pt + in_off(a.pt_off, a.pt_stride, p);
                 const uint32_t padn = O[16u * nb - 1u];       // PKCS7.unpad: n = data[-1]

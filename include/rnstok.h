@@ -13,6 +13,9 @@
  *   rt_encrypt*        Token.encrypt             RNS/Cryptography/Token.py:87-97
  *   rt_decrypt*        Token.verify_hmac+decrypt RNS/Cryptography/Token.py:77-84,100-114
  *   rt_token_len       token size arithmetic     Token.py:50 (TOKEN_OVERHEAD) + PKCS7.py:35-39
+ *   rt_hkdf*           RNS.Cryptography.hkdf     RNS/Cryptography/HKDF.py:35-62
+ *   rt_keyset_create_hkdf  per-packet keying     Identity.py:837-846 (hkdf -> Token(derived_key)),
+ *                                                Link.py handshake key derivation
  *
  * Conventions
  *  - No exceptions cross the boundary.  API misuse returns a negative RT_E_*
@@ -142,6 +145,35 @@ int rt_encrypt_host(const rt_keyset *ks, const uint8_t *pt, const uint64_t *pt_o
 int rt_decrypt_host(const rt_keyset *ks, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,
                     const uint32_t *key_idx, uint8_t *pt, const uint64_t *pt_off, uint32_t *pt_len,
                     int32_t *status, uint32_t n);
+
+/* ---- key derivation (RNS.Cryptography.hkdf, HKDF.py:35-62) -------------- */
+/* n independent HKDF-SHA256 derivations.  Item i: input key material
+ * ikm + i*ikm_stride (ikm_len bytes; 0 is allowed, as b"" is in the
+ * reference), salt + i*salt_stride (salt_len bytes; salt NULL or salt_len 0
+ * means the reference's default of 32 zero bytes, HKDF.py:45-46; salts over
+ * 64 bytes are hashed first as HMAC.py does with long keys), a context shared
+ * by all items (NULL / 0: empty, HKDF.py:48-49); `length` >= 1 output bytes
+ * are written at out + i*out_stride (length 0 is RT_E_INVAL, HKDF.py:40-41).
+ * Output blocks past 255 wrap the counter byte exactly as HKDF.py:60 does.
+ * rt_hkdf takes DEVICE pointers and only enqueues; rt_hkdf_host takes HOST
+ * pointers and returns when `out` is filled. */
+int rt_hkdf(rt_ctx *ctx, const uint8_t *ikm, uint64_t ikm_stride, uint32_t ikm_len,
+            const uint8_t *salt, uint64_t salt_stride, uint32_t salt_len,
+            const uint8_t *context, uint32_t context_len,
+            uint8_t *out, uint64_t out_stride, uint32_t length, uint32_t n, void *stream);
+int rt_hkdf_host(rt_ctx *ctx, const uint8_t *ikm, uint64_t ikm_stride, uint32_t ikm_len,
+                 const uint8_t *salt, uint64_t salt_stride, uint32_t salt_len,
+                 const uint8_t *context, uint32_t context_len,
+                 uint8_t *out, uint64_t out_stride, uint32_t length, uint32_t n);
+/* Per-packet keying: derive n token keys of key_len (64 or 32) bytes with
+ * HKDF (arguments as rt_hkdf, DEVICE pointers) and build their key tables,
+ * without the derived keys ever leaving the device: key i of the keyset is
+ * Token(hkdf(key_len, ikm_i, salt_i, context)) as Identity.encrypt /
+ * __decrypt construct it (Identity.py:837-846).  Encrypt with key_idx[i] = i. */
+rt_keyset *rt_keyset_create_hkdf(rt_ctx *ctx, const uint8_t *ikm, uint64_t ikm_stride, uint32_t ikm_len,
+                                 const uint8_t *salt, uint64_t salt_stride, uint32_t salt_len,
+                                 const uint8_t *context, uint32_t context_len, uint32_t key_len, uint32_t n,
+                                 void *stream);
 
 /* ---- memory helpers (so a non-torch host can drive the device API) ------- */
 void *rt_device_alloc(rt_ctx *ctx, uint64_t bytes);

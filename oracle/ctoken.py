@@ -39,6 +39,7 @@ def lib():
         L.oracle_aes_encrypt_block.argtypes = [vp, ctypes.c_uint32, vp, vp]
         L.oracle_aes_decrypt_block.argtypes = [vp, ctypes.c_uint32, vp, vp]
         L.oracle_sbox.argtypes = [vp]
+        L.oracle_hkdf.argtypes = [vp, ctypes.c_uint64, vp, ctypes.c_uint32, vp, ctypes.c_uint32, ctypes.c_uint64, vp]
         _lib = L
     return _lib
 
@@ -112,3 +113,16 @@ def decrypt_batch(keys, tok, tok_off, tok_len, key_idx, pt, pt_off, pt_len, stat
                                     _p(pt_off), _p(pt_len), _p(status), len(tok_off), threads)
     if rc:
         raise ValueError("oracle_decrypt_batch rc=%d" % rc)
+
+
+def hkdf(length, derive_from, salt=None, context=None):
+    """RNS/Cryptography/HKDF.py:35-62 (argument checks :40-44 included)."""
+    if length is None or length < 1:
+        raise ValueError("Invalid output key length")
+    if derive_from is None or derive_from == "":
+        raise ValueError("Cannot derive key from empty input material")
+    out = ctypes.create_string_buffer(length)
+    lib().oracle_hkdf(_buf(derive_from), len(derive_from), None if salt is None else _buf(salt),
+                      0 if salt is None else len(salt), None if context is None else _buf(context),
+                      0 if context is None else len(context), length, out)
+    return out.raw

@@ -23,6 +23,7 @@
  *   CBC chaining           RNS/Cryptography/aes/aes256.py:215-235
  *   AES-128 (32 B keys)    RNS/Cryptography/aes/aes128.py:156-326, AES.py:43-76
  *   HMAC (key pad, ipad/opad) RNS/Cryptography/HMAC.py:47-84,114-125
+ *   HKDF-SHA256            RNS/Cryptography/HKDF.py:35-62 (oracle_hkdf)
  *   SHA-256                hashlib.sha256 (third-party: CPython _hashlib over
  *                          OpenSSL 3.0.2), restated from FIPS 180-4.
  *
@@ -359,3 +360,30 @@ void oracle_aes_decrypt_block(const uint8_t *key, uint32_t klen, const uint8_t i
     memcpy(out, in, 16); aes_decrypt_block(rk, nr, out);
 }
 void oracle_sbox(uint8_t out[256]) { build_tables(); memcpy(out, SBOX, 256); }
+
+/* HKDF-SHA256 as RNS/Cryptography/HKDF.py:35-62 computes it:
+ *   salt NULL or empty -> 32 zero bytes (:45-46); context NULL -> b"" (:48-49)
+ *   PRK = HMAC(salt, ikm) (:51); T_i = HMAC(PRK, T_{i-1} || context || (i % 256)) (:56-60)
+ *   output = (T_1 || T_2 || ...)[:length] (:62)
+ * The argument checks (:40-44) belong to the caller (length >= 1, ikm given). */
+void oracle_hkdf(const uint8_t *ikm, uint64_t ikm_len, const uint8_t *salt, uint32_t salt_len,
+                 const uint8_t *context, uint32_t context_len, uint64_t length, uint8_t *out) {
+    static const uint8_t zeros[32] = {0};
+    if (!salt || salt_len == 0) { salt = zeros; salt_len = 32; }
+    uint8_t prk[32], t[32];
+    oracle_hmac_sha256(salt, salt_len, ikm, ikm_len, prk);
+    uint8_t *msg = (uint8_t *)malloc(32 + (size_t)context_len + 1);
+    uint64_t done = 0;
+    for (uint64_t i = 0; done < length; ++i) {
+        size_t m = 0;
+        if (i) { memcpy(msg, t, 32); m = 32; }
+        if (context_len) memcpy(msg + m, context, context_len);
+        m += context_len;
+        msg[m++] = (uint8_t)((i + 1) % 256);
+        oracle_hmac_sha256(prk, 32, msg, m, t);
+        uint64_t take = length - done < 32 ? length - done : 32;
+        memcpy(out + done, t, take);
+        done += take;
+    }
+    free(msg);
+}

@@ -1,0 +1,146 @@
+// hkdf_kernels.hip — batched HKDF-SHA256 (RNS/Cryptography/HKDF.py:35-62).
+//
+// Identity.encrypt / __decrypt derive a fresh 64-byte token key per packet
+// (Identity.py:837-846, salt = the identity hash, context None) and
+// Link.handshake one per link; the derived keys feed Token(key).  Here one
+// lane derives one key: the salt becomes the HMAC key (HMAC.py:73-82: zero
+// padded to 64 bytes, hashed first when longer), PRK = HMAC(salt, ikm), then
+// T_i = HMAC(PRK, T_{i-1} || context || i mod 256) with the PRK's ipad/opad
+// midstates computed once.  With 32-byte ikm, 16-byte salt, no context and a
+// 64-byte output that is 10 SHA-256 compressions per lane.
+//
+// The messages are assembled word by word from byte loads (global memory is
+// read once per byte; the previous block T_{i-1} comes from registers), so
+// any lengths work; this is VALU-bound like the token MAC.
+#include "token_device.h"
+#include "token_launch.h"
+
+namespace rnstok {
+
+namespace {
+
+__device__ const uint32_t SHA_IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                       0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+
+// Byte q of  seg[0..seg_len) || tail (if tail >= 0) || 0x80 || zeros.
+__device__ __forceinline__ uint32_t msg_byte(const uint8_t *seg, uint32_t seg_len, int tail, uint32_t q) {
+    const uint32_t body = seg_len + (tail >= 0 ? 1u : 0u);
+    if (q < seg_len) return seg[q];
+    if (q < body) return (uint32_t)tail;
+    return q == body ? 0x80u : 0u;
+}
+
+// SHA-256 of  pre[0..npre) words || seg || tail  appended to `prior` bytes
+// already absorbed into h (prior = 64 after an HMAC ipad/opad block), with
+// the final padding.  npre is 0 or 8 (the previous HKDF block).
+__device__ __forceinline__ void sha_msg(uint32_t h[8], uint32_t prior, const uint32_t pre[8], uint32_t npre,
+                                     const uint8_t *seg, uint32_t seg_len, int tail) {
+    const uint64_t m = 4ull * npre + seg_len + (tail >= 0 ? 1u : 0u);
+    const uint64_t bits = (prior + m) * 8ull;
+    const uint64_t nblk = (m + 8u) / 64u + 1u;
+    for (uint64_t b = 0; b < nblk; ++b) {
+        uint32_t w[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (b == 0 && (uint32_t)k < npre) {
+                w[k] = pre[k];
+            } else {
+                const uint32_t q = (uint32_t)(64u * b + 4u * k) - 4u * npre;
+                w[k] = (msg_byte(seg, seg_len, tail, q) << 24) | (msg_byte(seg, seg_len, tail, q + 1) << 16) |
+                       (msg_byte(seg, seg_len, tail, q + 2) << 8) | msg_byte(seg, seg_len, tail, q + 3);
+            }
+        }
+        if (b + 1 == nblk) {
+            w[14] = (uint32_t)(bits >> 32);
+            w[15] = (uint32_t)bits;
+        }
+        sha256_compress(h, w);
+    }
+}
+
+// HMAC ipad / opad midstates for a key (HMAC.py:73-82).
+__device__ __forceinline__ void hmac_midstates(const uint32_t key[16], uint32_t hi[8], uint32_t ho[8]) {
+    uint32_t wi[16], wo[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        wi[i] = key[i] ^ 0x36363636u;
+        wo[i] = key[i] ^ 0x5c5c5c5cu;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) hi[i] = ho[i] = SHA_IV[i];
+    sha256_compress(hi, wi);
+    sha256_compress(ho, wo);
+}
+
+__global__ __launch_bounds__(256) void k_hkdf(HkdfArgs a) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const uint8_t *ikm = a.ikm + (uint64_t)i * a.ikm_stride;
+    // HMAC key = salt; None / empty salt -> 32 zero bytes (HKDF.py:45-46), which
+    // zero-pads to the same 64-byte block as an empty key.
+    uint32_t key[16];
+    const uint32_t sl = a.salt ? a.salt_len : 0u;
+    const uint8_t *salt = a.salt ? a.salt + (uint64_t)i * a.salt_stride : nullptr;
+    if (sl > 64u) {                                   // HMAC.py: long keys are hashed first
+        uint32_t d[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d[k] = SHA_IV[k];
+        sha_msg(d, 0u, nullptr, 0u, salt, sl, -1);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) key[k] = k < 8 ? d[k] : 0u;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t q = 4u * k + j;
+                v = (v << 8) | (q < sl ? salt[q] : 0u);
+            }
+            key[k] = v;
+        }
+    }
+    uint32_t hi[8], ho[8], inner[8], prk[8];
+    hmac_midstates(key, hi, ho);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) inner[k] = hi[k];
+    sha_msg(inner, 64u, nullptr, 0u, ikm, a.ikm_len, -1);
+    hmac_outer(prk, inner, ho);                      // PRK = HMAC(salt, ikm)  (HKDF.py:51)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) key[k] = k < 8 ? prk[k] : 0u;
+    hmac_midstates(key, hi, ho);
+    uint32_t t[8];
+    uint8_t *out = a.out + (uint64_t)i * a.out_stride;
+    for (uint32_t blk = 0, done = 0; done < a.length; ++blk) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) inner[k] = hi[k];
+        // T_blk = HMAC(PRK, T_{blk-1} || context || (blk+1) % 256)  (HKDF.py:56-60)
+        sha_msg(inner, 64u, t, blk ? 8u : 0u, a.context, a.context_len, (int)((blk + 1u) & 255u));
+        hmac_outer(t, inner, ho);
+        const uint32_t take = a.length - done < 32u ? a.length - done : 32u;
+        if (take == 32u) {
+            st16(out + done, u32x4{bswap(t[0]), bswap(t[1]), bswap(t[2]), bswap(t[3])});
+            st16(out + done + 16, u32x4{bswap(t[4]), bswap(t[5]), bswap(t[6]), bswap(t[7])});
+        } else {
+            for (uint32_t j = 0; j < take; ++j) {
+                uint32_t wv = t[0];
+#pragma unroll
+                for (int k = 1; k < 8; ++k)
+                    if ((j >> 2) == (uint32_t)k) wv = t[k];
+                out[done + j] = (uint8_t)(wv >> (24u - 8u * (j & 3u)));
+            }
+        }
+        done += take;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_hkdf(const HkdfArgs &a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    const uint32_t threads = 256;
+    hipLaunchKernelGGL(k_hkdf, dim3((a.n + threads - 1) / threads), dim3(threads), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace rnstok

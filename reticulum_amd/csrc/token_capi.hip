@@ -415,6 +415,105 @@ int rt_decrypt_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_
     return RT_OK;
 }
 
+
+// ------------------------------------------------------------------ HKDF --
+
+static int hkdf_check(rt_ctx *c, const uint8_t *ikm, uint32_t ikm_len, const uint8_t *context, uint32_t context_len,
+                      uint32_t length) {
+    if (!c) return fail(RT_E_INVAL, "null context");
+    if (length < 1) return fail(RT_E_INVAL, "Invalid output key length");          // HKDF.py:40-41
+    if (ikm_len && !ikm) return fail(RT_E_INVAL, "Cannot derive key from empty input material");   // HKDF.py:43-44
+    if (context_len && !context) return fail(RT_E_INVAL, "rt_hkdf: null context bytes");
+    return RT_OK;
+}
+
+static HkdfArgs hkdf_args(const uint8_t *ikm, uint64_t ikm_stride, uint32_t ikm_len, const uint8_t *salt,
+                          uint64_t salt_stride, uint32_t salt_len, const uint8_t *context, uint32_t context_len,
+                          uint8_t *out, uint64_t out_stride, uint32_t length, uint32_t n) {
+    HkdfArgs a{};
+    a.ikm = ikm; a.ikm_stride = ikm_stride; a.ikm_len = ikm_len;
+    a.salt = salt_len ? salt : nullptr; a.salt_stride = salt_stride; a.salt_len = salt ? salt_len : 0;
+    a.context = context_len ? context : nullptr; a.context_len = context ? context_len : 0;
+    a.out = out; a.out_stride = out_stride; a.length = length; a.n = n;
+    return a;
+}
+
+int rt_hkdf(rt_ctx *c, const uint8_t *ikm, uint64_t ikm_stride, uint32_t ikm_len, const uint8_t *salt,
+            uint64_t salt_stride, uint32_t salt_len, const uint8_t *context, uint32_t context_len, uint8_t *out,
+            uint64_t out_stride, uint32_t length, uint32_t n, void *stream) {
+    int rc = hkdf_check(c, ikm, ikm_len, context, context_len, length);
+    if (rc || n == 0) return rc;
+    if (!out) return fail(RT_E_INVAL, "rt_hkdf: null output");
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    const HkdfArgs a = hkdf_args(ikm, ikm_stride, ikm_len, salt, salt_stride, salt_len, context, context_len, out,
+                                 out_stride, length, n);
+    RT_HIP(launch_hkdf(a, pick(c, stream)), "hkdf launch");
+    return RT_OK;
+}
+
+int rt_hkdf_host(rt_ctx *c, const uint8_t *ikm, uint64_t ikm_stride, uint32_t ikm_len, const uint8_t *salt,
+                 uint64_t salt_stride, uint32_t salt_len, const uint8_t *context, uint32_t context_len, uint8_t *out,
+                 uint64_t out_stride, uint32_t length, uint32_t n) {
+    int rc = hkdf_check(c, ikm, ikm_len, context, context_len, length);
+    if (rc || n == 0) return rc;
+    if (!out) return fail(RT_E_INVAL, "rt_hkdf: null output");
+    if (!salt) salt_len = 0;
+    if (!context) context_len = 0;
+    // packed copies on the device: ikm n x ikm_len, salt n x salt_len, context, out n x length
+    const uint64_t b_ikm = (uint64_t)n * ikm_len, b_salt = (uint64_t)n * salt_len, b_out = (uint64_t)n * length;
+    const uint64_t o_ikm = 0, o_salt = align16(o_ikm + b_ikm), o_ctx = align16(o_salt + b_salt),
+                   o_out = align16(o_ctx + context_len), total = align16(o_out + b_out);
+    std::lock_guard<std::mutex> g(c->mu);
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    if ((rc = ensure_work(c, total))) return rc;
+    uint8_t *w = c->d_work;
+    hipStream_t s = c->stream;
+    if (b_ikm)
+        RT_HIP(hipMemcpy2DAsync(w + o_ikm, ikm_len, ikm, ikm_stride, ikm_len, n, hipMemcpyHostToDevice, s), "H2D ikm");
+    if (b_salt)
+        RT_HIP(hipMemcpy2DAsync(w + o_salt, salt_len, salt, salt_stride, salt_len, n, hipMemcpyHostToDevice, s),
+               "H2D salt");
+    if (context_len) RT_HIP(hipMemcpyAsync(w + o_ctx, context, context_len, hipMemcpyHostToDevice, s), "H2D context");
+    const HkdfArgs a = hkdf_args(w + o_ikm, ikm_len, ikm_len, b_salt ? w + o_salt : nullptr, salt_len, salt_len,
+                                 context_len ? w + o_ctx : nullptr, context_len, w + o_out, length, length, n);
+    RT_HIP(launch_hkdf(a, s), "hkdf launch");
+    RT_HIP(hipMemcpy2DAsync(out, out_stride, w + o_out, length, length, n, hipMemcpyDeviceToHost, s), "D2H out");
+    RT_HIP(hipStreamSynchronize(s), "stream sync");
+    return RT_OK;
+}
+
+rt_keyset *rt_keyset_create_hkdf(rt_ctx *c, const uint8_t *ikm, uint64_t ikm_stride, uint32_t ikm_len,
+                                 const uint8_t *salt, uint64_t salt_stride, uint32_t salt_len,
+                                 const uint8_t *context, uint32_t context_len, uint32_t key_len, uint32_t n,
+                                 void *stream) {
+    if (hkdf_check(c, ikm, ikm_len, context, context_len, key_len)) return nullptr;
+    if (n == 0) {
+        fail(RT_E_INVAL, "rt_keyset_create_hkdf: zero keys");
+        return nullptr;
+    }
+    if (key_len != 64 && key_len != 32) {   // Token.py:72
+        fail(RT_E_INVAL, "Token key must be 128 or 256 bits, not " + std::to_string(key_len * 8));
+        return nullptr;
+    }
+    hipSetDevice(c->device);
+    hipStream_t s = pick(c, stream);
+    uint8_t *d_keys = nullptr;
+    if (hipMallocAsync((void **)&d_keys, (uint64_t)n * key_len, s) != hipSuccess) {
+        fail(RT_E_NOMEM, "derived key buffer allocation failed");
+        return nullptr;
+    }
+    const HkdfArgs a = hkdf_args(ikm, ikm_stride, ikm_len, salt, salt_stride, salt_len, context, context_len, d_keys,
+                                 key_len, key_len, n);
+    rt_keyset *k = nullptr;
+    hipError_t e = launch_hkdf(a, s);
+    if (e == hipSuccess)
+        k = rt_keyset_create_device(c, d_keys, key_len, n, s);
+    else
+        hip_fail(e, "hkdf launch");
+    hipFreeAsync(d_keys, s);     // stream-ordered: freed after the key setup has consumed it
+    return k;
+}
+
 // ------------------------------------------------------------------ memory
 
 void *rt_device_alloc(rt_ctx *c, uint64_t bytes) {

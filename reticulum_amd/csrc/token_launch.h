@@ -40,6 +40,24 @@ struct DecArgs {
     uint32_t n;
 };
 
+// HKDF-SHA256 over n items (hkdf_kernels.hip): item i reads ikm + i*ikm_stride
+// and salt + i*salt_stride (salt null or salt_len 0: zero key), shares the
+// context, writes `length` bytes at out + i*out_stride.
+struct HkdfArgs {
+    const uint8_t *ikm;
+    uint64_t ikm_stride;
+    uint32_t ikm_len;
+    const uint8_t *salt;
+    uint64_t salt_stride;
+    uint32_t salt_len;
+    const uint8_t *context;
+    uint32_t context_len;
+    uint8_t *out;
+    uint64_t out_stride;
+    uint32_t length;
+    uint32_t n;
+};
+
 hipError_t configure_kernels();
 
 // Length bucketing: order[] = packet indices grouped by descending AES quad
@@ -51,6 +69,7 @@ hipError_t launch_length_order(const uint32_t *len, uint32_t n, int dec, void *w
                                int n_cu, hipStream_t s);
 hipError_t launch_encrypt(const EncArgs &a, int nr, int n_cu, hipStream_t s);
 hipError_t launch_decrypt(const DecArgs &a, int nr, int n_cu, hipStream_t s);
+hipError_t launch_hkdf(const HkdfArgs &a, hipStream_t s);
 hipError_t launch_key_setup(const uint8_t *keys, uint32_t key_len, uint32_t n_keys, const uint8_t *sbox,
                             uint32_t *rec, hipStream_t s);
 

@@ -93,3 +93,39 @@ def decrypt(ks: KeySet, tok, tok_off, tok_len, pt, pt_off, out_len, status, key_
         return
     _native.check(lib.rt_decrypt(ks.handle, _p(tok), _p(tok_off), _p(tok_len), _p(key_idx), _p(pt), _p(pt_off),
                                  _p(out_len), _p(status), n, _stream(stream)))
+
+
+def hkdf(ikm, out, salt=None, context=None, stream=None):
+    """HKDF-SHA256 over device rows (RNS/Cryptography/HKDF.py:35-62): ikm
+    (n, L) uint8, salt (n, S) uint8 or None (the reference's 32 zero bytes),
+    context a (C,) uint8 device tensor or None, out (n, length) uint8 with
+    length = out.shape[1] >= 1.  Row i of out = hkdf(length, ikm[i], salt[i],
+    context)."""
+    _check_u8(ikm, out, salt, context)
+    n = ikm.shape[0]
+    if out.shape[0] != n or (salt is not None and salt.shape[0] != n):
+        raise ValueError("shape mismatch")
+    length = out.shape[1]
+    lib = _native.load()
+    ctx = _native.context(out.device.index)
+    _native.check(lib.rt_hkdf(ctx, _p(ikm), ikm.stride(0), ikm.shape[1], _p(salt),
+                              salt.stride(0) if salt is not None else 0, salt.shape[1] if salt is not None else 0,
+                              _p(context), context.numel() if context is not None else 0, _p(out), out.stride(0),
+                              length, n, _stream(stream)))
+
+
+def derive_keyset(ikm, salt=None, context=None, key_len=64, stream=None):
+    """Per-packet keying from device rows (Identity.py:837-846): KeySet whose
+    key i is Token(hkdf(key_len, ikm[i], salt[i], context)); derived and
+    expanded on the device."""
+    _check_u8(ikm, salt, context)
+    n = ikm.shape[0]
+    lib = _native.load()
+    ctx = _native.context(ikm.device.index)
+    h = lib.rt_keyset_create_hkdf(ctx, _p(ikm), ikm.stride(0), ikm.shape[1], _p(salt),
+                                  salt.stride(0) if salt is not None else 0, salt.shape[1] if salt is not None else 0,
+                                  _p(context), context.numel() if context is not None else 0, key_len, n,
+                                  _stream(stream))
+    if not h:
+        raise _native.NativeError(-1, _native.last_error())
+    return KeySet._adopt(h, key_len, n, lib, ctx)

@@ -114,6 +114,13 @@ class KeySet:
         if not self._ptr:
             raise _native.NativeError(-1, _native.last_error())
 
+    @classmethod
+    def _adopt(cls, handle, key_len, n_keys, lib, ctx):
+        """Wrap a keyset handle built by the library (e.g. rt_keyset_create_hkdf)."""
+        ks = cls.__new__(cls)
+        ks.key_len, ks.n_keys, ks._lib, ks._ctx, ks._ptr = key_len, n_keys, lib, ctx, handle
+        return ks
+
     @property
     def handle(self):
         return self._ptr

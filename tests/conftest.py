@@ -10,6 +10,7 @@ for p in (ROOT, TESTS):
         sys.path.insert(0, p)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden", "token_vectors.json")
+GOLDEN_HKDF = os.path.join(ROOT, "tests", "golden", "hkdf_vectors.json")
 
 
 def pytest_configure(config):
@@ -21,4 +22,11 @@ def pytest_configure(config):
 def golden():
     import json
     with open(GOLDEN) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def golden_hkdf():
+    import json
+    with open(GOLDEN_HKDF) as f:
         return json.load(f)

@@ -90,6 +90,21 @@ class FakeLib:
                 pbuf[region] = 0
         return 0
 
+    def rt_hkdf_host(self, ctx, ikm, ikm_stride, ikm_len, salt, salt_stride, salt_len, context, context_len, out,
+                     out_stride, length, n):
+        self.calls.append(("rt_hkdf_host", ikm_len, salt_len, n))
+        if length < 1:
+            return -1
+        a = _arr(ikm, np.uint8, ikm_stride * (n - 1) + ikm_len) if ikm_len else None
+        s = _arr(salt, np.uint8, salt_stride * (n - 1) + salt_len) if salt_len and salt else None
+        c = _arr(context, np.uint8, context_len).tobytes() if context_len else None
+        o = _arr(out, np.uint8, out_stride * (n - 1) + length)
+        for i in range(n):
+            k = a[i * ikm_stride:i * ikm_stride + ikm_len].tobytes() if ikm_len else b""
+            sl = s[i * salt_stride:i * salt_stride + salt_len].tobytes() if s is not None else None
+            o[i * out_stride:i * out_stride + length] = np.frombuffer(ctoken.hkdf(length, k, sl, c), np.uint8)
+        return 0
+
 
 def _raw_last_byte(key, tok):
     """Last byte of the CBC-decrypted body (for BAD_PAD detail)."""

@@ -1,0 +1,152 @@
+"""HKDF-SHA256 (RNS/Cryptography/HKDF.py:35-62) and per-packet keying
+(Identity.py:837-846).
+
+CPU: the C oracle against the golden vectors made from the reference
+(tests/golden/gen_hkdf.py), including the derivation the reference performs
+while decrypting its own identity KAT (tests/identity.py:11-19,148-158); the
+host layer's argument errors and batching logic (fake library).
+GPU (-m gpu): the k_hkdf kernel through the C-ABI, bit-exact against the same
+vectors and the oracle, and the derived-keyset path end to end.
+"""
+import numpy as np
+import pytest
+
+import reticulum_amd as rt
+from oracle import ctoken
+from tests_helpers import b
+
+
+def _h(x):
+    return None if x is None else bytes.fromhex(x)
+
+
+@pytest.fixture
+def fake(monkeypatch):
+    import fake_native
+    return fake_native.install(monkeypatch)
+
+
+# ------------------------------------------------------------------ oracle --
+
+def test_oracle_hkdf_vectors(golden_hkdf):
+    for v in golden_hkdf["vectors"]:
+        assert ctoken.hkdf(v["length"], _h(v["ikm"]), _h(v["salt"]), _h(v["context"])).hex() == v["okm"], v["note"]
+    bt = golden_hkdf["batch"]
+    for ikm, salt, okm in zip(bt["ikm"], bt["salt"], bt["okm"]):
+        assert ctoken.hkdf(bt["length"], b(ikm), b(salt)).hex() == okm
+
+
+def test_oracle_hkdf_identity_kat(golden_hkdf, golden):
+    """The reference's own derivation while decrypting fixed_token: the okm is
+    the token key captured in token_vectors.json, and it opens the token."""
+    k = golden_hkdf["identity_kat"]
+    okm = ctoken.hkdf(k["length"], b(k["ikm"]), _h(k["salt"]), _h(k["context"]))
+    assert okm.hex() == k["okm"] == golden["kat"]["fixed_token"]["derived_key"]
+    st, pt = ctoken.decrypt(okm, b(golden["kat"]["fixed_token"]["token"]))
+    assert st == 0 and pt.hex() == golden["kat"]["fixed_token"]["pt"]
+
+
+def test_oracle_hkdf_errors(golden_hkdf):
+    for e in golden_hkdf["errors"]:
+        ikm = None if e["derive_from"] is None else ("" if e["derive_from"] == "str:" else b(e["derive_from"]))
+        with pytest.raises(ValueError) as ex:
+            ctoken.hkdf(e["length"], ikm)
+        assert str(ex.value) == e["msg"]
+
+
+# -------------------------------------------------------------- host layer --
+
+def test_hkdf_argument_errors_match_reference(golden_hkdf):
+    """Raised before any native call, with the reference's messages."""
+    for e in golden_hkdf["errors"]:
+        ikm = None if e["derive_from"] is None else ("" if e["derive_from"] == "str:" else b(e["derive_from"]))
+        with pytest.raises(ValueError) as ex:
+            rt.hkdf(length=e["length"], derive_from=ikm)
+        assert str(ex.value) == e["msg"]
+        with pytest.raises(ValueError):
+            rt.hkdf_batch(e["length"], [ikm] if ikm is not None else None)
+    with pytest.raises(TypeError):
+        rt.hkdf(length=3, derive_from=b"abc", context="x")      # bytes + str in the reference
+    with pytest.raises(ValueError):
+        rt.derive_keyset([b"x" * 32], key_len=48)
+
+
+def test_hkdf_host_layer_groups_mixed_lengths(fake, golden_hkdf):
+    """Mixed ikm / salt lengths (salt None, b"" and bytes) are split into
+    uniform launches and reassembled in order."""
+    vs = [v for v in golden_hkdf["vectors"] if v["context"] is None and v["length"] == 64]
+    ikm = [_h(v["ikm"]) for v in vs]
+    salt = [_h(v["salt"]) for v in vs]
+    out = rt.hkdf_batch(64, ikm, salt)
+    assert [o.tobytes().hex() for o in out] == [v["okm"] for v in vs]
+    launches = [c for c in fake.calls if c[0] == "rt_hkdf_host"]
+    assert len(launches) == len({(len(i), 0 if s is None else len(s)) for i, s in zip(ikm, salt)})
+    for v in golden_hkdf["vectors"]:
+        assert rt.hkdf(v["length"], _h(v["ikm"]), _h(v["salt"]), _h(v["context"])).hex() == v["okm"], v["note"]
+
+
+# --------------------------------------------------------------------- GPU --
+
+@pytest.mark.gpu
+def test_gpu_hkdf_golden(golden_hkdf):
+    for v in golden_hkdf["vectors"]:
+        assert rt.hkdf(v["length"], _h(v["ikm"]), _h(v["salt"]), _h(v["context"])).hex() == v["okm"], v["note"]
+    bt = golden_hkdf["batch"]
+    out = rt.hkdf_batch(bt["length"], [b(x) for x in bt["ikm"]], [b(x) for x in bt["salt"]])
+    assert [o.tobytes().hex() for o in out] == bt["okm"]
+    k = golden_hkdf["identity_kat"]
+    assert rt.hkdf(k["length"], b(k["ikm"]), _h(k["salt"]), _h(k["context"])).hex() == k["okm"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("salt_len,ctx_len,length", [(16, 0, 64), (0, 0, 32), (100, 30, 200), (64, 1, 33)])
+def test_gpu_hkdf_device_batch_vs_oracle(salt_len, ctx_len, length):
+    import torch
+    from reticulum_amd import device
+    rng = np.random.Generator(np.random.PCG64(salt_len * 7 + ctx_len + length))
+    n = 3000
+    ikm = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    salt = rng.integers(0, 256, (n, salt_len), dtype=np.uint8) if salt_len else None
+    ctxb = rng.integers(0, 256, ctx_len, dtype=np.uint8).tobytes() if ctx_len else None
+    out = torch.zeros((n, length), dtype=torch.uint8, device="cuda")
+    device.hkdf(torch.from_numpy(ikm).cuda(), out, None if salt is None else torch.from_numpy(salt).cuda(),
+                None if ctxb is None else torch.frombuffer(bytearray(ctxb), dtype=torch.uint8).cuda())
+    got = out.cpu().numpy()
+    for i in range(0, n, 97):
+        ref = ctoken.hkdf(length, ikm[i].tobytes(), None if salt is None else salt[i].tobytes(), ctxb)
+        assert got[i].tobytes() == ref, i
+
+
+@pytest.mark.gpu
+def test_gpu_derived_keyset_identity_kat(golden_hkdf, golden):
+    """Identity.__decrypt's derivation + Token on the device: the keyset
+    derived from the reference KAT's shared key and identity-hash salt opens
+    the reference's fixed_token."""
+    k = golden_hkdf["identity_kat"]
+    ks = rt.derive_keyset([b(k["ikm"])], [b(k["salt"])], key_len=64)
+    pts, st = ks.decrypt_batch([b(golden["kat"]["fixed_token"]["token"])])
+    assert int(st[0]) == 0 and pts[0].hex() == golden["kat"]["fixed_token"]["pt"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key_len", [64, 32])
+def test_gpu_derived_keyset_per_packet_tokens(key_len):
+    """Per-packet keying at batch scale: key i = hkdf(key_len, ikm_i, salt_i);
+    tokens with key_idx = i match the oracle with the oracle's derived keys."""
+    import torch
+    from reticulum_amd import device
+    rng = np.random.Generator(np.random.PCG64(key_len))
+    n, L = 4096, 383                        # Packet.ENCRYPTED_MDU
+    ikm = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    salt = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    ks = device.derive_keyset(torch.from_numpy(ikm).cuda(), torch.from_numpy(salt).cuda(), key_len=key_len)
+    pt = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    iv = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    tl = rt.token_len(L)
+    tok = torch.empty((n, tl), dtype=torch.uint8, device="cuda")
+    kidx = torch.arange(n, dtype=torch.int32, device="cuda")
+    device.encrypt_uniform(ks, torch.from_numpy(pt).cuda(), L, torch.from_numpy(iv).cuda(), tok, key_idx=kidx)
+    th = tok.cpu().numpy()
+    for i in range(0, n, 61):
+        key = ctoken.hkdf(key_len, ikm[i].tobytes(), salt[i].tobytes())
+        assert th[i].tobytes() == ctoken.encrypt(key, iv[i].tobytes(), pt[i].tobytes()), i

@@ -14,6 +14,9 @@
  *   rt_decrypt*        Token.verify_hmac+decrypt RNS/Cryptography/Token.py:77-84,100-114
  *   rt_token_len       token size arithmetic     Token.py:50 (TOKEN_OVERHEAD) + PKCS7.py:35-39
  *   rt_hkdf*           RNS.Cryptography.hkdf     RNS/Cryptography/HKDF.py:35-62
+ *   rt_map_hashes /    Resource hashmap          RNS/Resource.py:426-468 (map hashes + the
+ *   rt_resource_hashmap_host                      collision guard), get_map_hash :505-506,
+ *                                                receive_part :865-866
  *   rt_keyset_create_hkdf  per-packet keying     Identity.py:837-846 (hkdf -> Token(derived_key)),
  *                                                Link.py handshake key derivation
  *
@@ -174,6 +177,29 @@ rt_keyset *rt_keyset_create_hkdf(rt_ctx *ctx, const uint8_t *ikm, uint64_t ikm_s
                                  const uint8_t *salt, uint64_t salt_stride, uint32_t salt_len,
                                  const uint8_t *context, uint32_t context_len, uint32_t key_len, uint32_t n,
                                  void *stream);
+
+/* ---- Resource hashmap (RNS/Resource.py:426-468, 505-506) ---------------- */
+/* map_hash_j = SHA-256(part_j || salt)[:4] for n_parts parts, DEVICE pointers.
+ * Part j is data + part_off[j] (part_len[j] bytes) when part_off/part_len are
+ * given, else the uniform segmentation of one resource that the sender uses:
+ * data[j*sdu, min((j+1)*sdu, size)) with n_parts = ceil(size / sdu).  The
+ * salt is the resource's random_hash (RANDOM_HASH_SIZE = 4 bytes): salts +
+ * part_res[j]*salt_len (part_res NULL: every part uses salts[0..salt_len)).
+ * map_hashes receives 4 bytes per part (MAPHASH_LEN).  If first_collision is
+ * not NULL it receives, per resource, the first (batch-wide) part index whose map hash
+ * equals one of the previous `guard` map hashes of the same resource
+ * (ResourceAdvertisement.COLLISION_GUARD_SIZE = 224 in the reference), or
+ * 0xFFFFFFFF: the point where the reference's loop breaks to draw a new
+ * random_hash.  Parts of one resource must be contiguous and in order. */
+int rt_map_hashes(rt_ctx *ctx, const uint8_t *data, const uint64_t *part_off, const uint32_t *part_len,
+                  uint64_t size, uint32_t sdu, const uint8_t *salts, uint32_t salt_len, const uint32_t *part_res,
+                  uint32_t n_res, uint32_t guard, uint8_t *map_hashes, uint32_t *first_collision, uint32_t n_parts,
+                  void *stream);
+/* One resource in HOST memory (uniform segmentation); returns when the
+ * hashmap (4*ceil(size/sdu) bytes) and *first_collision are written. */
+int rt_resource_hashmap_host(rt_ctx *ctx, const uint8_t *data, uint64_t size, uint32_t sdu,
+                             const uint8_t *random_hash, uint32_t rh_len, uint32_t guard, uint8_t *hashmap,
+                             uint32_t *first_collision);
 
 /* ---- memory helpers (so a non-torch host can drive the device API) ------- */
 void *rt_device_alloc(rt_ctx *ctx, uint64_t bytes);

@@ -126,3 +126,25 @@ def hkdf(length, derive_from, salt=None, context=None):
                       0 if salt is None else len(salt), None if context is None else _buf(context),
                       0 if context is None else len(context), length, out)
     return out.raw
+
+
+def map_hashes(stream, random_hash, sdu):
+    """Resource map hashes, RNS/Resource.py:505-506 (get_map_hash) over the
+    sender's segmentation :449-451: SHA-256(part || random_hash)[:4] each."""
+    n = -(-len(stream) // sdu)
+    return b"".join(sha256(stream[i * sdu:(i + 1) * sdu] + random_hash)[:4] for i in range(n))
+
+
+def first_collision(hashes, guard):
+    """Index where the hashmap loop of RNS/Resource.py:446-462 breaks: the
+    first map hash equal to one of the previous `guard` map hashes; None if
+    the hashmap is accepted."""
+    window = []
+    for i in range(len(hashes) // 4):
+        mh = hashes[4 * i:4 * i + 4]
+        if mh in window:
+            return i
+        window.append(mh)
+        if len(window) > guard:
+            window.pop(0)
+    return None

@@ -416,6 +416,63 @@ int rt_decrypt_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_
 }
 
 
+// --------------------------------------------------------- Resource hashmap --
+
+int rt_map_hashes(rt_ctx *c, const uint8_t *data, const uint64_t *part_off, const uint32_t *part_len, uint64_t size,
+                  uint32_t sdu, const uint8_t *salts, uint32_t salt_len, const uint32_t *part_res, uint32_t n_res,
+                  uint32_t guard, uint8_t *map_hashes, uint32_t *first_collision, uint32_t n_parts, void *stream) {
+    if (!c) return fail(RT_E_INVAL, "null context");
+    if (n_parts == 0) return RT_OK;
+    if (!data || !map_hashes) return fail(RT_E_INVAL, "rt_map_hashes: null data or output");
+    if ((part_off == nullptr) != (part_len == nullptr))
+        return fail(RT_E_INVAL, "rt_map_hashes: part_off and part_len go together");
+    if (!part_off) {
+        if (sdu == 0 || (size + sdu - 1) / sdu != n_parts)
+            return fail(RT_E_INVAL, "rt_map_hashes: n_parts must be ceil(size / sdu)");
+        if (part_res) return fail(RT_E_INVAL, "rt_map_hashes: uniform segmentation is one resource");
+    }
+    if (salt_len && !salts) return fail(RT_E_INVAL, "rt_map_hashes: null salts");
+    if (n_res == 0) n_res = 1;
+    MapArgs m{};
+    m.data = data; m.part_off = part_off; m.part_len = part_len; m.size = size; m.sdu = sdu;
+    m.salts = salts; m.salt_len = salts ? salt_len : 0; m.part_res = part_res; m.n_res = n_res; m.guard = guard;
+    m.out = map_hashes; m.first_collision = first_collision; m.n_parts = n_parts;
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    RT_HIP(launch_map_hashes(m, pick(c, stream)), "map hash launch");
+    return RT_OK;
+}
+
+int rt_resource_hashmap_host(rt_ctx *c, const uint8_t *data, uint64_t size, uint32_t sdu, const uint8_t *random_hash,
+                             uint32_t rh_len, uint32_t guard, uint8_t *hashmap, uint32_t *first_collision) {
+    if (!c) return fail(RT_E_INVAL, "null context");
+    if (sdu == 0) return fail(RT_E_INVAL, "rt_resource_hashmap_host: sdu must be > 0");
+    const uint64_t parts = (size + sdu - 1) / sdu;
+    if (parts > 0xffffffffull) return fail(RT_E_INVAL, "rt_resource_hashmap_host: too many parts");
+    if (first_collision) *first_collision = 0xffffffffu;
+    if (parts == 0) return RT_OK;
+    if (!data || !hashmap || (rh_len && !random_hash)) return fail(RT_E_INVAL, "rt_resource_hashmap_host: null buffer");
+    const uint64_t o_data = 0, o_salt = align16(size), o_out = align16(o_salt + rh_len),
+                   o_col = align16(o_out + 4 * parts), total = align16(o_col + 4);
+    std::lock_guard<std::mutex> g(c->mu);
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    int rc = ensure_work(c, total);
+    if (rc) return rc;
+    uint8_t *w = c->d_work;
+    hipStream_t s = c->stream;
+    RT_HIP(hipMemcpyAsync(w + o_data, data, size, hipMemcpyHostToDevice, s), "H2D data");
+    if (rh_len) RT_HIP(hipMemcpyAsync(w + o_salt, random_hash, rh_len, hipMemcpyHostToDevice, s), "H2D salt");
+    MapArgs m{};
+    m.data = w + o_data; m.size = size; m.sdu = sdu; m.salts = w + o_salt; m.salt_len = rh_len; m.n_res = 1;
+    m.guard = guard; m.out = w + o_out; m.first_collision = (uint32_t *)(w + o_col); m.n_parts = (uint32_t)parts;
+    RT_HIP(launch_map_hashes(m, s), "map hash launch");
+    RT_HIP(hipMemcpyAsync(hashmap, w + o_out, 4 * parts, hipMemcpyDeviceToHost, s), "D2H hashmap");
+    uint32_t col = 0xffffffffu;
+    RT_HIP(hipMemcpyAsync(&col, w + o_col, 4, hipMemcpyDeviceToHost, s), "D2H collision");
+    RT_HIP(hipStreamSynchronize(s), "stream sync");
+    if (first_collision) *first_collision = col;
+    return RT_OK;
+}
+
 // ------------------------------------------------------------------ HKDF --
 
 static int hkdf_check(rt_ctx *c, const uint8_t *ikm, uint32_t ikm_len, const uint8_t *context, uint32_t context_len,

@@ -695,70 +695,88 @@ hipError_t launch_length_order(const uint32_t *len, uint32_t n, int dec, void *w
 
 // ------------------------------------------------------------- key setup --
 
-__device__ __forceinline__ uint32_t sub_word(const uint8_t *sbox, uint32_t w) {
-    return (uint32_t)sbox[w & 255u] | ((uint32_t)sbox[(w >> 8) & 255u] << 8) |
-           ((uint32_t)sbox[(w >> 16) & 255u] << 16) | ((uint32_t)sbox[w >> 24] << 24);
+// Packed GF(2^8) doubling of the four bytes of a word (xtime, aes256.py:86).
+__device__ __forceinline__ uint32_t xt4(uint32_t x) {
+    return ((x & 0x7f7f7f7fu) << 1) ^ (((x >> 7) & 0x01010101u) * 0x1bu);
 }
-__device__ __forceinline__ uint32_t inv_mix_word(uint32_t w) {
-    uint32_t a0 = w & 255u, a1 = (w >> 8) & 255u, a2 = (w >> 16) & 255u, a3 = w >> 24;
-    uint32_t b0 = gmul(a0, 14) ^ gmul(a1, 11) ^ gmul(a2, 13) ^ gmul(a3, 9);
-    uint32_t b1 = gmul(a1, 14) ^ gmul(a2, 11) ^ gmul(a3, 13) ^ gmul(a0, 9);
-    uint32_t b2 = gmul(a2, 14) ^ gmul(a3, 11) ^ gmul(a0, 13) ^ gmul(a1, 9);
-    uint32_t b3 = gmul(a3, 14) ^ gmul(a0, 11) ^ gmul(a1, 13) ^ gmul(a2, 9);
-    return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+// InvMixColumns of one column (aes256.py:101 inv_mix_columns): byte i of the
+// result is 14*a_i ^ 11*a_{i+1} ^ 13*a_{i+2} ^ 9*a_{i+3}.
+__device__ __forceinline__ uint32_t inv_mix_word(uint32_t x) {
+    const uint32_t x2 = xt4(x), x4 = xt4(x2), x8 = xt4(x4);
+    return (x8 ^ x4 ^ x2) ^ rotr(x8 ^ x2 ^ x, 8) ^ rotr(x8 ^ x4 ^ x, 16) ^ rotr(x8 ^ x, 24);
+}
+__device__ __forceinline__ uint32_t sub_word(const uint8_t *sb, uint32_t w) {
+    return (uint32_t)sb[w & 255u] | ((uint32_t)sb[(w >> 8) & 255u] << 8) | ((uint32_t)sb[(w >> 16) & 255u] << 16) |
+           ((uint32_t)sb[w >> 24] << 24);
 }
 
-__global__ __launch_bounds__(256) void k_key_setup(const uint8_t *keys, uint32_t key_len, uint32_t n_keys,
-                                                    const uint8_t *sbox, uint32_t *rec_out) {
+// One lane per key; NK = 8 (64-byte keys, AES-256) or 4 (32-byte keys, AES-128).
+template <int NK>
+__global__ __launch_bounds__(256) void k_key_setup(const uint8_t *keys, uint32_t n_keys, const uint8_t *sbox,
+                                                    uint32_t *rec_out) {
+    __shared__ uint8_t sb[256];
+    sb[threadIdx.x] = sbox[threadIdx.x];          // blockDim.x == 256
+    __syncthreads();
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_keys) return;
-    const uint8_t *key = keys + (uint64_t)k * key_len;
-    uint32_t *rec = rec_out + (uint64_t)k * REC_WORDS;
-    const uint32_t half = key_len / 2;          // sk = key[:half], ek = key[half:]  (Token.py:61-70)
-    const uint8_t *ek = key + half;
-    const int nk = (int)half / 4, nr = nk + 6, total = 4 * (nr + 1);
-    uint32_t w[60];
-    for (int i = 0; i < nk; ++i)
+    constexpr int HALF = 4 * NK, NR = NK + 6, TOTAL = 4 * (NR + 1);
+    const uint8_t *key = keys + (uint64_t)k * (2 * HALF);
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    v4u *rec = (v4u *)(rec_out + (uint64_t)k * REC_WORDS);      // 544-byte records, 16-byte aligned
+    const uint8_t *ek = key + HALF;                              // sk = key[:HALF], ek = key[HALF:]  (Token.py:61-70)
+    uint32_t w[TOTAL];
+#pragma unroll
+    for (int i = 0; i < NK; ++i)
         w[i] = (uint32_t)ek[4 * i] | ((uint32_t)ek[4 * i + 1] << 8) | ((uint32_t)ek[4 * i + 2] << 16) |
                ((uint32_t)ek[4 * i + 3] << 24);
     uint32_t rcon = 1;
-    for (int i = nk; i < total; ++i) {
+#pragma unroll
+    for (int i = NK; i < TOTAL; ++i) {          // aes256.py:146-175 (aes128.py for NK = 4)
         uint32_t t = w[i - 1];
-        if (i % nk == 0) {
-            t = sub_word(sbox, (t >> 8) | (t << 24)) ^ rcon;    // RotWord then SubWord, Rcon in byte 0
-            rcon = xt(rcon);
-        } else if (nk > 6 && i % nk == 4) {
-            t = sub_word(sbox, t);
+        if (i % NK == 0) {
+            t = sub_word(sb, (t >> 8) | (t << 24)) ^ rcon;      // RotWord, SubWord, Rcon in byte 0
+            rcon = xt4(rcon);
+        } else if (NK > 6 && i % NK == 4) {
+            t = sub_word(sb, t);
         }
-        w[i] = w[i - nk] ^ t;
+        w[i] = w[i - NK] ^ t;
     }
-    for (int i = 0; i < 60; ++i) rec[REC_ENC + i] = i < total ? w[i] : 0u;
+#pragma unroll
+    for (int q = 0; q < 15; ++q)
+        rec[(REC_ENC >> 2) + q] = 4 * q < TOTAL ? v4u{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]} : v4u{0, 0, 0, 0};
     // equivalent inverse cipher: dk[0] = rk[nr], dk[r] = InvMix(rk[nr-r]), dk[nr] = rk[0]
-    for (int r = 0; r <= nr; ++r)
-        for (int j = 0; j < 4; ++j) {
-            uint32_t v = w[4 * (nr - r) + j];
-            rec[REC_DEC + 4 * r + j] = (r == 0 || r == nr) ? v : inv_mix_word(v);
+#pragma unroll
+    for (int r = 0; r < 15; ++r) {
+        v4u d = {0, 0, 0, 0};
+        if (r <= NR) {
+            const int o = 4 * (NR - r);
+            d = (r == 0 || r == NR) ? v4u{w[o], w[o + 1], w[o + 2], w[o + 3]}
+                                    : v4u{inv_mix_word(w[o]), inv_mix_word(w[o + 1]), inv_mix_word(w[o + 2]),
+                                          inv_mix_word(w[o + 3])};
         }
-    for (int i = 4 * (nr + 1); i < 60; ++i) rec[REC_DEC + i] = 0u;
+        rec[(REC_DEC >> 2) + r] = d;
+    }
     // HMAC midstates (HMAC.py:73-82): sk zero-padded to 64 B, ^0x36 / ^0x5c
-    uint32_t blk[16], hi[8], ho[8];
+    uint32_t bi[16], bo[16], hi[8], ho[8];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        uint32_t v = 0;
+        if (4 * i < HALF)
+            v = ((uint32_t)key[4 * i] << 24) | ((uint32_t)key[4 * i + 1] << 16) | ((uint32_t)key[4 * i + 2] << 8) |
+                key[4 * i + 3];
+        bi[i] = v ^ 0x36363636u;
+        bo[i] = v ^ 0x5c5c5c5cu;
+    }
     const uint32_t iv0[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                              0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-    for (int pass = 0; pass < 2; ++pass) {
-        const uint32_t x = pass ? 0x5c5c5c5cu : 0x36363636u;
-        for (int i = 0; i < 16; ++i) {
-            uint32_t v = 0;
-            for (int b = 0; b < 4; ++b) {
-                uint32_t idx = 4 * i + b;
-                v = (v << 8) | (idx < half ? key[idx] : 0u);
-            }
-            blk[i] = v ^ x;
-        }
-        uint32_t *hs = pass ? ho : hi;
-        for (int i = 0; i < 8; ++i) hs[i] = iv0[i];
-        sha256_compress(hs, blk);
-    }
-    for (int i = 0; i < 8; ++i) { rec[REC_IPAD + i] = hi[i]; rec[REC_OPAD + i] = ho[i]; }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) hi[i] = ho[i] = iv0[i];
+    sha256_compress(hi, bi);
+    sha256_compress(ho, bo);
+    rec[REC_IPAD >> 2] = v4u{hi[0], hi[1], hi[2], hi[3]};
+    rec[(REC_IPAD >> 2) + 1] = v4u{hi[4], hi[5], hi[6], hi[7]};
+    rec[REC_OPAD >> 2] = v4u{ho[0], ho[1], ho[2], ho[3]};
+    rec[(REC_OPAD >> 2) + 1] = v4u{ho[4], ho[5], ho[6], ho[7]};
 }
 
 // --------------------------------------------------------------- launchers --
@@ -844,7 +862,10 @@ hipError_t launch_decrypt(const DecArgs &a, int nr, int n_cu, hipStream_t s) {
 }
 hipError_t launch_key_setup(const uint8_t *keys, uint32_t key_len, uint32_t n_keys, const uint8_t *sbox,
                             uint32_t *rec, hipStream_t s) {
-    hipLaunchKernelGGL(k_key_setup, dim3((n_keys + 255) / 256), dim3(256), 0, s, keys, key_len, n_keys, sbox, rec);
+    if (key_len == 64)
+        hipLaunchKernelGGL(k_key_setup<8>, dim3((n_keys + 255) / 256), dim3(256), 0, s, keys, n_keys, sbox, rec);
+    else
+        hipLaunchKernelGGL(k_key_setup<4>, dim3((n_keys + 255) / 256), dim3(256), 0, s, keys, n_keys, sbox, rec);
     return hipGetLastError();
 }
 hipError_t configure_kernels() {

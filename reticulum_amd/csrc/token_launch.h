@@ -58,6 +58,25 @@ struct HkdfArgs {
     uint32_t n;
 };
 
+// Resource map hashes (resource_kernels.hip): part j = data + part_off[j]
+// (part_len[j] bytes), or with part_off null the uniform segmentation
+// data[j*sdu, min((j+1)*sdu, size)); salt = salts + part_res[j]*salt_len.
+struct MapArgs {
+    const uint8_t *data;
+    const uint64_t *part_off;
+    const uint32_t *part_len;
+    uint64_t size;
+    uint32_t sdu;
+    const uint8_t *salts;
+    uint32_t salt_len;
+    const uint32_t *part_res;
+    uint32_t n_res;
+    uint32_t guard;
+    uint8_t *out;                  // 4 bytes per part
+    uint32_t *first_collision;     // n_res entries or null
+    uint32_t n_parts;
+};
+
 hipError_t configure_kernels();
 
 // Length bucketing: order[] = packet indices grouped by descending AES quad
@@ -69,6 +88,7 @@ hipError_t launch_length_order(const uint32_t *len, uint32_t n, int dec, void *w
                                int n_cu, hipStream_t s);
 hipError_t launch_encrypt(const EncArgs &a, int nr, int n_cu, hipStream_t s);
 hipError_t launch_decrypt(const DecArgs &a, int nr, int n_cu, hipStream_t s);
+hipError_t launch_map_hashes(const MapArgs &m, hipStream_t s);
 hipError_t launch_hkdf(const HkdfArgs &a, hipStream_t s);
 hipError_t launch_key_setup(const uint8_t *keys, uint32_t key_len, uint32_t n_keys, const uint8_t *sbox,
                             uint32_t *rec, hipStream_t s);

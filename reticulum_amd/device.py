@@ -129,3 +129,21 @@ def derive_keyset(ikm, salt=None, context=None, key_len=64, stream=None):
     if not h:
         raise _native.NativeError(-1, _native.last_error())
     return KeySet._adopt(h, key_len, n, lib, ctx)
+
+
+def map_hashes(data, out, salts, part_off=None, part_len=None, part_res=None, sdu=464, guard=0,
+               first_collision=None, stream=None):
+    """Resource map hashes over device buffers (Resource.py:505-506): out
+    (n_parts*4,) uint8; salts (n_res, S) uint8 (random hashes); with
+    part_off (int64) / part_len (int32) the parts are arbitrary slices of
+    ``data`` and part_res (int32) names each part's resource, otherwise
+    ``data`` is one resource cut into ``sdu``-byte parts.  first_collision
+    (n_res,) int32 receives the first part index repeating a map hash of the
+    previous ``guard`` parts, or -1."""
+    _check_u8(data, out, salts)
+    n_parts = out.numel() // 4
+    lib = _native.load()
+    ctx = _native.context(data.device.index)
+    _native.check(lib.rt_map_hashes(ctx, _p(data), _p(part_off), _p(part_len), data.numel(), sdu, _p(salts),
+                                    salts.shape[1], _p(part_res), salts.shape[0], guard, _p(out),
+                                    _p(first_collision), n_parts, _stream(stream)))

@@ -90,6 +90,16 @@ class FakeLib:
                 pbuf[region] = 0
         return 0
 
+    def rt_resource_hashmap_host(self, ctx, data, size, sdu, rh, rh_len, guard, hashmap, first_collision):
+        self.calls.append(("rt_resource_hashmap_host", size, sdu, guard))
+        stream = _arr(data, np.uint8, size).tobytes()
+        salt = _arr(rh, np.uint8, rh_len).tobytes() if rh_len else b""
+        hm = ctoken.map_hashes(stream, salt, sdu)
+        _arr(hashmap, np.uint8, len(hm))[:] = np.frombuffer(hm, np.uint8)
+        col = ctoken.first_collision(hm, guard) if guard else None
+        first_collision._obj.value = 0xFFFFFFFF if col is None else col
+        return 0
+
     def rt_hkdf_host(self, ctx, ikm, ikm_stride, ikm_len, salt, salt_stride, salt_len, context, context_len, out,
                      out_stride, length, n):
         self.calls.append(("rt_hkdf_host", ikm_len, salt_len, n))

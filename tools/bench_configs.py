@@ -5,6 +5,10 @@
 c3  : 2^20 x 500 B, 65 536 per-packet keys (uniform random key_idx)
 c4  : 262 144 x 16 KiB, one key (Resource-sized tokens, whole batch on 1 GPU)
 c4s8: 32 768 x 16 KiB, one key (the per-GPU shard of c4 at 8 GPUs)
+ident: 2^20 x 500 B with a fresh HKDF-derived key per packet (Identity.encrypt
+      keying, Identity.py:837-846): times rt_hkdf (32 B shared key, 16 B
+      salt -> 64 B), the derived keyset (HKDF + key setup, incl. allocation)
+      and encrypt / decrypt with key_idx = packet index
 c5  : 2^20 packets (the per-GPU share of 8 M at 8 GPUs), lengths uniform in
       64..4096 B, 65 536 keys, 50/50 encrypt / decrypt (decrypt inputs are
       valid tokens produced by the encrypt kernel beforehand)
@@ -44,6 +48,43 @@ def main():
         keys = torch.randint(0, 256, (nk, 64), dtype=torch.uint8).numpy()
         ks = rt.KeySet(keys)
         kidx = torch.randint(0, nk, (n,), dtype=torch.int32, device=dev, generator=g) if nk > 1 else None
+        tok = torch.empty((n, tl), dtype=torch.uint8, device=dev)
+        back = torch.empty((n, tl - 48), dtype=torch.uint8, device=dev)
+        ol = torch.empty(n, dtype=torch.int32, device=dev)
+        st = torch.empty(n, dtype=torch.int32, device=dev)
+
+        def enc():
+            device.encrypt_uniform(ks, pt, L, iv, tok, key_idx=kidx)
+
+        def dec():
+            device.decrypt_uniform(ks, tok, tl, back, ol, st, key_idx=kidx)
+
+        bytes_pt = n * L
+        n_enc = n_dec = n
+        check = lambda: bool((st == 0).all()) and torch.equal(back[:, :L], pt)  # noqa: E731
+    elif cfg == "ident":
+        n, L = 1 << 20, 500
+        tl = rt.token_len(L)
+        ikm = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device=dev, generator=g)
+        salt = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
+        okm = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        hk, dk = [], []
+        for _ in range(5):
+            e0.record()
+            device.hkdf(ikm, okm, salt)
+            e1.record()
+            ks = device.derive_keyset(ikm, salt)
+            e2.record()
+            torch.cuda.synchronize()
+            hk.append(e0.elapsed_time(e1))
+            dk.append(e1.elapsed_time(e2))
+        res["hkdf_ms"] = sorted(hk)[2]
+        res["derive_keyset_ms"] = sorted(dk)[2]
+        res["hkdf_keys_s"] = n / (res["hkdf_ms"] * 1e-3)
+        pt = torch.randint(0, 256, (n, L), dtype=torch.uint8, device=dev, generator=g)
+        iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
+        kidx = torch.arange(n, dtype=torch.int32, device=dev)
         tok = torch.empty((n, tl), dtype=torch.uint8, device=dev)
         back = torch.empty((n, tl - 48), dtype=torch.uint8, device=dev)
         ol = torch.empty(n, dtype=torch.int32, device=dev)

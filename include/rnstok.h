@@ -17,6 +17,12 @@
  *   rt_map_hashes /    Resource hashmap          RNS/Resource.py:426-468 (map hashes + the
  *   rt_resource_hashmap_host                      collision guard), get_map_hash :505-506,
  *                                                receive_part :865-866
+ *   rt_hdlc_frame      HDLC.escape + framing     RNS/Interfaces/TCPInterface.py:44-53, :323
+ *   rt_hdlc_deframe    HDLC read loop            RNS/Interfaces/TCPInterface.py:387-410, :336-339
+ *   rt_ifac_mask       IFAC on transmit          RNS/Transport.py:1069-1101
+ *   rt_ifac_unmask     IFAC on inbound           RNS/Transport.py:1441-1475
+ *   rt_packet_unpack   Packet.unpack + get_hash  RNS/Packet.py:236-268, 342-353
+ *   rt_packet_pack_headers  Packet.pack header   RNS/Packet.py:167-228
  *   rt_keyset_create_hkdf  per-packet keying     Identity.py:837-846 (hkdf -> Token(derived_key)),
  *                                                Link.py handshake key derivation
  *
@@ -200,6 +206,73 @@ int rt_map_hashes(rt_ctx *ctx, const uint8_t *data, const uint64_t *part_off, co
 int rt_resource_hashmap_host(rt_ctx *ctx, const uint8_t *data, uint64_t size, uint32_t sdu,
                              const uint8_t *random_hash, uint32_t rh_len, uint32_t guard, uint8_t *hashmap,
                              uint32_t *first_collision);
+
+/* ---- wire-side neighbours (framing, IFAC, packet header) --------------- */
+/* HDLC framing of n packets into one stream, in order: frame i is
+ * 7E || escape(packet i) || 7E (escape: 7D -> 7D 5D, 7E -> 7D 5E) at
+ * out + frame_off[i]; frame_off has n+1 entries, frame_off[n] = total bytes.
+ * out needs at most sum(2*len+2) bytes.  DEVICE pointers; `workspace` of
+ * rt_hdlc_frame_workspace_bytes(n) bytes. */
+uint64_t rt_hdlc_frame_workspace_bytes(uint32_t n);
+int rt_hdlc_frame(rt_ctx *ctx, const uint8_t *pkt, const uint64_t *pkt_off, const uint32_t *pkt_len, uint32_t n,
+                  uint8_t *out, uint64_t *frame_off, void *workspace, void *stream);
+/* One pass of the HDLC read loop over buf[0, len) (everything received so
+ * far).  For every pair of consecutive 7E flags k, k+1 (at most max_pairs):
+ * the frame between them, unescaped with the loop's two replace passes, is
+ * written at out + frame_off[k] (its position in buf, so `out` needs len
+ * bytes), frame_len[k] bytes, and status[k] is RT_FRAME_OK (handed to
+ * process_incoming), RT_FRAME_BAD_LEN (dropped by check_frame_len: length <=
+ * HEADER_MINSIZE = 19 or > hw_mtu + ifac_size) or RT_FRAME_EMPTY (skipped).
+ * counts[0] = number of pairs, counts[1] = bytes consumed: the loop keeps
+ * buf[counts[1], len) for the next read (all of it is dropped when no flag is
+ * present or the tail from the last flag exceeds 2*hw_mtu).  DEVICE
+ * pointers; `workspace` of rt_hdlc_deframe_workspace_bytes(len) bytes. */
+#define RT_FRAME_OK      0
+#define RT_FRAME_BAD_LEN 1
+#define RT_FRAME_EMPTY   2
+uint64_t rt_hdlc_deframe_workspace_bytes(uint64_t len);
+int rt_hdlc_deframe(rt_ctx *ctx, const uint8_t *buf, uint64_t len, uint32_t hw_mtu, uint32_t ifac_size, uint8_t *out,
+                    uint64_t *frame_off, uint32_t *frame_len, int32_t *status, uint64_t *counts, uint64_t max_pairs,
+                    void *workspace, void *stream);
+/* IFAC on transmit: packet i (pkt + pkt_off[i], pkt_len[i] >= 2 bytes) with
+ * its access code ifac + i*ifac_size (the last ifac_size bytes of the
+ * interface identity's Ed25519 signature of the packet, computed by the
+ * caller; signing stays on the host) becomes pkt_len[i] + ifac_size bytes at
+ * out + out_off[i]: IFAC flag set, IFAC inserted after the 2 header bytes,
+ * all but the IFAC masked with HKDF(len + ifac_size, ifac, ifac_key).
+ * ifac_key: key_len (<= 64) bytes shared by the batch.  DEVICE pointers. */
+int rt_ifac_mask(rt_ctx *ctx, const uint8_t *pkt, const uint64_t *pkt_off, const uint32_t *pkt_len,
+                 const uint8_t *ifac, uint32_t ifac_size, const uint8_t *ifac_key, uint32_t key_len, uint8_t *out,
+                 const uint64_t *out_off, uint32_t n, void *stream);
+/* IFAC on inbound: status[i] = 0 when the packet carries the IFAC flag and
+ * is longer than 2 + ifac_size; then its IFAC goes to ifac_out + i*ifac_size
+ * and the unmasked packet without it (pkt_len[i] - ifac_size bytes, flag
+ * cleared) to out + out_off[i].  status 1: the reference drops the packet
+ * before signing.  The caller then compares ifac with the tail of
+ * sign(unmasked packet) (Transport.py:1477-1481). */
+int rt_ifac_unmask(rt_ctx *ctx, const uint8_t *pkt, const uint64_t *pkt_off, const uint32_t *pkt_len,
+                   uint32_t ifac_size, const uint8_t *ifac_key, uint32_t key_len, uint8_t *ifac_out, uint8_t *out,
+                   const uint64_t *out_off, int32_t *status, uint32_t n, void *stream);
+/* Packet.unpack + get_hash per packet (96 bytes).  ok = 0 where unpack
+ * returns False (hop count >= 128, packet too short for its header). */
+typedef struct rt_packet_fields {
+    uint8_t  ok, flags, hops, header_type, context_flag, transport_type, destination_type, packet_type;
+    uint8_t  context, reserved[3];
+    uint32_t data_offset, data_len;     /* data = packet[data_offset : data_offset + data_len] */
+    uint8_t  transport_id[16];          /* HEADER_2 only */
+    uint8_t  destination_hash[16];
+    uint8_t  packet_hash[32];           /* SHA-256(flags & 0x0F || packet[2 or 18:]) */
+    uint8_t  reserved2[12];
+} rt_packet_fields;
+int rt_packet_unpack(rt_ctx *ctx, const uint8_t *pkt, const uint64_t *pkt_off, const uint32_t *pkt_len,
+                     rt_packet_fields *fields, uint32_t n, void *stream);
+/* Packet.pack's header for n packets at out + out_off[i]: flags, hops (NULL:
+ * 0), [transport_id (16 B each; NULL: HEADER_1 for all)], destination hash
+ * (16 B each), context — 19 or 35 bytes; the payload (a token from
+ * rt_encrypt, written at out_off[i] + header length) follows. */
+int rt_packet_pack_headers(rt_ctx *ctx, const uint8_t *flags, const uint8_t *hops, const uint8_t *transport_id,
+                           const uint8_t *destination_hash, const uint8_t *context, uint8_t *out,
+                           const uint64_t *out_off, uint32_t n, void *stream);
 
 /* ---- memory helpers (so a non-torch host can drive the device API) ------- */
 void *rt_device_alloc(rt_ctx *ctx, uint64_t bytes);

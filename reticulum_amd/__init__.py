@@ -13,12 +13,14 @@ Batch use: ``KeySet.encrypt_batch`` / ``decrypt_batch`` over host buffers,
 ``hkdf`` (drop-in for RNS.Cryptography.hkdf), ``hkdf_batch`` and
 ``derive_keyset`` (Identity's per-packet keys, derived and expanded on the
 device).  Resource hashmaps: ``resource_hashmap`` / ``build_hashmap`` /
-``get_map_hash`` (Resource.py:426-468, 505-506).
+``get_map_hash`` (Resource.py:426-468, 505-506).  Wire-side neighbours
+(HDLC framing, IFAC masking, packet header unpack/pack): ``reticulum_amd.wire``.
 """
 from ._native import NativeError, NativeUnavailable, LIB_PATH  # noqa: F401
 from ._native import RT_ST_OK, RT_ST_TOO_SHORT, RT_ST_BAD_HMAC, RT_ST_BAD_CT_LEN, RT_ST_BAD_PAD  # noqa: F401
 from .hkdf import derive_keyset, hkdf, hkdf_batch  # noqa: F401
 from .resource import build_hashmap, get_map_hash, resource_hashmap  # noqa: F401
+from . import wire  # noqa: F401
 from .token import AES, AES_128_CBC, AES_256_CBC, KeySet, Packed, Token, TOKEN_OVERHEAD, token_len  # noqa: F401
 
 __version__ = "0.1.0"

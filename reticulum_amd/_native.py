@@ -43,6 +43,14 @@ SIGNATURES = [
     ("rt_keyset_create_hkdf", _vp, [_vp, _vp, _u64, _u32, _vp, _u64, _u32, _vp, _u32, _u32, _u32, _vp]),
     ("rt_map_hashes", _int, [_vp, _vp, _vp, _vp, _u64, _u32, _vp, _u32, _vp, _u32, _u32, _vp, _vp, _u32, _vp]),
     ("rt_resource_hashmap_host", _int, [_vp, _vp, _u64, _u32, _vp, _u32, _u32, _vp, _vp]),
+    ("rt_hdlc_frame_workspace_bytes", _u64, [_u32]),
+    ("rt_hdlc_frame", _int, [_vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp]),
+    ("rt_hdlc_deframe_workspace_bytes", _u64, [_u64]),
+    ("rt_hdlc_deframe", _int, [_vp, _vp, _u64, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp]),
+    ("rt_ifac_mask", _int, [_vp, _vp, _vp, _vp, _vp, _u32, _vp, _u32, _vp, _vp, _u32, _vp]),
+    ("rt_ifac_unmask", _int, [_vp, _vp, _vp, _vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp]),
+    ("rt_packet_unpack", _int, [_vp, _vp, _vp, _vp, _vp, _u32, _vp]),
+    ("rt_packet_pack_headers", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),
     ("rt_device_alloc", _vp, [_vp, _u64]),
     ("rt_device_free", None, [_vp, _vp]),
     ("rt_host_alloc", _vp, [_u64]),

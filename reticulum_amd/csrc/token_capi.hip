@@ -416,6 +416,92 @@ int rt_decrypt_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_
 }
 
 
+// ------------------------------------------------------------------ wire --
+
+static_assert(sizeof(rt_packet_fields) == 96, "rt_packet_fields layout");
+
+uint64_t rt_hdlc_frame_workspace_bytes(uint32_t n) { return hdlc_frame_workspace_bytes(n); }
+uint64_t rt_hdlc_deframe_workspace_bytes(uint64_t len) { return hdlc_deframe_workspace_bytes(len); }
+
+int rt_hdlc_frame(rt_ctx *c, const uint8_t *pkt, const uint64_t *pkt_off, const uint32_t *pkt_len, uint32_t n,
+                  uint8_t *out, uint64_t *frame_off, void *workspace, void *stream) {
+    if (!c) return fail(RT_E_INVAL, "null context");
+    if (!frame_off) return fail(RT_E_INVAL, "rt_hdlc_frame: null frame_off");
+    if (n == 0) return RT_OK;
+    if (!pkt || !pkt_off || !pkt_len || !out || !workspace) return fail(RT_E_INVAL, "rt_hdlc_frame: null buffer");
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    RT_HIP(launch_hdlc_frame(pkt, pkt_off, pkt_len, n, out, frame_off, workspace, pick(c, stream)), "hdlc frame");
+    return RT_OK;
+}
+
+int rt_hdlc_deframe(rt_ctx *c, const uint8_t *buf, uint64_t len, uint32_t hw_mtu, uint32_t ifac_size, uint8_t *out,
+                    uint64_t *frame_off, uint32_t *frame_len, int32_t *status, uint64_t *counts, uint64_t max_pairs,
+                    void *workspace, void *stream) {
+    if (!c) return fail(RT_E_INVAL, "null context");
+    if (!counts || !workspace) return fail(RT_E_INVAL, "rt_hdlc_deframe: null counts/workspace");
+    if (len && (!buf || !out)) return fail(RT_E_INVAL, "rt_hdlc_deframe: null buffer");
+    if (max_pairs && (!frame_off || !frame_len || !status)) return fail(RT_E_INVAL, "rt_hdlc_deframe: null frame arrays");
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    RT_HIP(launch_hdlc_deframe(buf, len, hw_mtu, ifac_size, out, frame_off, frame_len, status, counts, max_pairs,
+                               workspace, pick(c, stream)),
+           "hdlc deframe");
+    return RT_OK;
+}
+
+int rt_ifac_mask(rt_ctx *c, const uint8_t *pkt, const uint64_t *pkt_off, const uint32_t *pkt_len, const uint8_t *ifac,
+                 uint32_t ifac_size, const uint8_t *ifac_key, uint32_t key_len, uint8_t *out, const uint64_t *out_off,
+                 uint32_t n, void *stream) {
+    if (!c) return fail(RT_E_INVAL, "null context");
+    if (key_len > 64) return fail(RT_E_INVAL, "rt_ifac_mask: ifac_key longer than 64 bytes");
+    if (ifac_size == 0 || ifac_size > 64) return fail(RT_E_INVAL, "rt_ifac_mask: ifac_size must be 1..64");
+    if (n == 0) return RT_OK;
+    if (!pkt || !pkt_off || !pkt_len || !ifac || !out || !out_off || (key_len && !ifac_key))
+        return fail(RT_E_INVAL, "rt_ifac_mask: null buffer");
+    IfacArgs a{pkt, pkt_off, pkt_len, const_cast<uint8_t *>(ifac), ifac_size, ifac_key, key_len, out, out_off,
+               nullptr, n};
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    RT_HIP(launch_ifac(a, true, pick(c, stream)), "ifac mask");
+    return RT_OK;
+}
+
+int rt_ifac_unmask(rt_ctx *c, const uint8_t *pkt, const uint64_t *pkt_off, const uint32_t *pkt_len, uint32_t ifac_size,
+                   const uint8_t *ifac_key, uint32_t key_len, uint8_t *ifac_out, uint8_t *out, const uint64_t *out_off,
+                   int32_t *status, uint32_t n, void *stream) {
+    if (!c) return fail(RT_E_INVAL, "null context");
+    if (key_len > 64) return fail(RT_E_INVAL, "rt_ifac_unmask: ifac_key longer than 64 bytes");
+    if (ifac_size == 0 || ifac_size > 64) return fail(RT_E_INVAL, "rt_ifac_unmask: ifac_size must be 1..64");
+    if (n == 0) return RT_OK;
+    if (!pkt || !pkt_off || !pkt_len || !ifac_out || !out || !out_off || !status || (key_len && !ifac_key))
+        return fail(RT_E_INVAL, "rt_ifac_unmask: null buffer");
+    IfacArgs a{pkt, pkt_off, pkt_len, ifac_out, ifac_size, ifac_key, key_len, out, out_off, status, n};
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    RT_HIP(launch_ifac(a, false, pick(c, stream)), "ifac unmask");
+    return RT_OK;
+}
+
+int rt_packet_unpack(rt_ctx *c, const uint8_t *pkt, const uint64_t *pkt_off, const uint32_t *pkt_len,
+                     rt_packet_fields *fields, uint32_t n, void *stream) {
+    if (!c) return fail(RT_E_INVAL, "null context");
+    if (n == 0) return RT_OK;
+    if (!pkt || !pkt_off || !pkt_len || !fields) return fail(RT_E_INVAL, "rt_packet_unpack: null buffer");
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    RT_HIP(launch_unpack(pkt, pkt_off, pkt_len, fields, n, pick(c, stream)), "packet unpack");
+    return RT_OK;
+}
+
+int rt_packet_pack_headers(rt_ctx *c, const uint8_t *flags, const uint8_t *hops, const uint8_t *transport_id,
+                           const uint8_t *destination_hash, const uint8_t *context, uint8_t *out,
+                           const uint64_t *out_off, uint32_t n, void *stream) {
+    if (!c) return fail(RT_E_INVAL, "null context");
+    if (n == 0) return RT_OK;
+    if (!flags || !destination_hash || !context || !out || !out_off)
+        return fail(RT_E_INVAL, "rt_packet_pack_headers: null buffer");
+    PackArgs a{flags, hops, context, destination_hash, transport_id, out, out_off, n};
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    RT_HIP(launch_pack_headers(a, pick(c, stream)), "pack headers");
+    return RT_OK;
+}
+
 // --------------------------------------------------------- Resource hashmap --
 
 int rt_map_hashes(rt_ctx *c, const uint8_t *data, const uint64_t *part_off, const uint32_t *part_len, uint64_t size,

@@ -77,6 +77,40 @@ struct MapArgs {
     uint32_t n_parts;
 };
 
+// Wire-side neighbours (wire_kernels.hip).
+struct IfacArgs {
+    const uint8_t *pkt;
+    const uint64_t *pkt_off;
+    const uint32_t *pkt_len;
+    uint8_t *ifac;                 // mask: input (n x ifac_size); unmask: output
+    uint32_t ifac_size;
+    const uint8_t *ifac_key;
+    uint32_t key_len;
+    uint8_t *out;
+    const uint64_t *out_off;
+    int32_t *status;               // unmask only
+    uint32_t n;
+};
+struct PackArgs {
+    const uint8_t *flags, *hops, *context;
+    const uint8_t *destination_hash;   // 16 B per packet
+    const uint8_t *transport_id;       // 16 B per packet or null (HEADER_1)
+    uint8_t *out;
+    const uint64_t *out_off;
+    uint32_t n;
+};
+uint64_t hdlc_frame_workspace_bytes(uint32_t n);
+uint64_t hdlc_deframe_workspace_bytes(uint64_t len);
+hipError_t launch_hdlc_frame(const uint8_t *pkt, const uint64_t *off, const uint32_t *len, uint32_t n, uint8_t *out,
+                             uint64_t *frame_off, void *ws, hipStream_t s);
+hipError_t launch_hdlc_deframe(const uint8_t *buf, uint64_t len, uint32_t hw_mtu, uint32_t ifac_size, uint8_t *out,
+                               uint64_t *frame_off, uint32_t *frame_len, int32_t *status, uint64_t *counts,
+                               uint64_t max_pairs, void *ws, hipStream_t s);
+hipError_t launch_ifac(const IfacArgs &a, bool mask, hipStream_t s);
+hipError_t launch_unpack(const uint8_t *pkt, const uint64_t *off, const uint32_t *len, void *fields, uint32_t n,
+                         hipStream_t s);
+hipError_t launch_pack_headers(const PackArgs &a, hipStream_t s);
+
 hipError_t configure_kernels();
 
 // Length bucketing: order[] = packet indices grouped by descending AES quad

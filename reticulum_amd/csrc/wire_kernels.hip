@@ -1,0 +1,516 @@
+// wire_kernels.hip — the wire-side neighbours of the token path.
+//
+// Inbound a node turns a byte stream from a socket into packets: HDLC
+// deframing (TCPInterface.py:387-410), IFAC unmasking (Transport.py:1441-1475),
+// header unpack and packet hash (Packet.py:236-268, 342-353), then the token
+// decrypt.  Outbound is the mirror: header pack (Packet.py:167-228), token
+// encrypt, IFAC masking (Transport.py:1069-1101), HDLC framing
+// (TCPInterface.py:44-53, 323).  These are byte-granular, per-packet
+// branchy transforms: one lane per packet (or per frame), HBM/latency-bound;
+// the only SHA-heavy pieces are the IFAC mask (an HKDF stream as long as the
+// packet) and the packet hash.
+//
+// Kernels:
+//   k_scan_*         exclusive prefix sums (u64) for frame placement
+//   k_hdlc_count     escaped frame length per packet
+//   k_hdlc_write     7E || escape(packet) || 7E at its prefix-sum offset
+//   k_flag_count / k_flag_scatter   positions of every 7E in a stream
+//   k_hdlc_unescape  one lane per consecutive flag pair: the read loop's two
+//                    bytes.replace passes, check_frame_len, empty-frame skip
+//   k_ifac           mask (outbound) / unmask (inbound) with HKDF(ifac, ifac_key)
+//   k_unpack         header fields + SHA-256 packet hash
+//   k_pack_headers   flags, hops, [transport id], destination hash, context
+#include "token_device.h"
+#include "token_launch.h"
+#include "../../include/rnstok.h"
+
+namespace rnstok {
+
+namespace {
+
+constexpr uint8_t FLAG = 0x7E, ESC = 0x7D, ESC_MASK = 0x20;
+constexpr uint32_t HEADER_MINSIZE = 19, DST_LEN = 16, PATHFINDER_M = 128;
+constexpr uint32_t SCAN_BLOCK = 1024;
+
+__device__ const uint32_t SHA_IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                       0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+
+// ------------------------------------------------------------------ scan --
+
+__device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t *total) {
+    __shared__ uint64_t sh[SCAN_BLOCK];
+    const uint32_t t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < blockDim.x; d <<= 1) {
+        const uint64_t add = t >= d ? sh[t - d] : 0;
+        __syncthreads();
+        sh[t] += add;
+        __syncthreads();
+    }
+    const uint64_t incl = sh[t];
+    *total = sh[blockDim.x - 1];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_block(const uint64_t *in, uint64_t *out, uint64_t *part,
+                                                           uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * SCAN_BLOCK + threadIdx.x;
+    uint64_t tot;
+    const uint64_t ex = block_exclusive_scan(i < n ? in[i] : 0, &tot);
+    if (i < n) out[i] = ex;
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+// one workgroup: exclusive scan of the block totals in place, total at part[nb]
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_parts(uint64_t *part, uint64_t nb) {
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < nb; base += SCAN_BLOCK) {
+        const uint64_t i = base + threadIdx.x;
+        uint64_t tot;
+        const uint64_t ex = block_exclusive_scan(i < nb ? part[i] : 0, &tot);
+        if (i < nb) part[i] = ex + carry;
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[nb] = carry;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_add(uint64_t *out, const uint64_t *part, uint64_t n,
+                                                         uint64_t *total_out) {
+    const uint64_t i = (uint64_t)blockIdx.x * SCAN_BLOCK + threadIdx.x;
+    if (i < n) out[i] += part[blockIdx.x];
+    if (total_out && i == 0) *total_out = part[(n + SCAN_BLOCK - 1) / SCAN_BLOCK];
+}
+
+// ------------------------------------------------------------- framing --
+
+__global__ __launch_bounds__(256) void k_hdlc_count(const uint8_t *pkt, const uint64_t *off, const uint32_t *len,
+                                                    uint64_t *flen, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t *p = pkt + off[i];
+    const uint32_t L = len[i];
+    uint32_t extra = 0;
+    for (uint32_t k = 0; k < L; ++k) extra += (p[k] == FLAG || p[k] == ESC);
+    flen[i] = 2ull + L + extra;                      // 7E || escape(p) || 7E
+}
+
+__global__ __launch_bounds__(256) void k_hdlc_write(const uint8_t *pkt, const uint64_t *off, const uint32_t *len,
+                                                    const uint64_t *foff, uint8_t *out, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t *p = pkt + off[i];
+    uint8_t *o = out + foff[i];
+    const uint32_t L = len[i];
+    uint64_t w = 0;
+    o[w++] = FLAG;
+    for (uint32_t k = 0; k < L; ++k) {       // HDLC.escape: ESC first, then FLAG (TCPInterface.py:50-52)
+        const uint8_t b = p[k];
+        if (b == ESC || b == FLAG) {
+            o[w++] = ESC;
+            o[w++] = b ^ ESC_MASK;
+        } else {
+            o[w++] = b;
+        }
+    }
+    o[w] = FLAG;
+}
+
+// ----------------------------------------------------------- deframing --
+
+constexpr uint32_t FLAG_CHUNK = 4096;        // stream bytes per workgroup (256 threads x 16)
+
+__global__ __launch_bounds__(256) void k_flag_count(const uint8_t *buf, uint64_t len, uint64_t *cnt) {
+    const uint64_t base = (uint64_t)blockIdx.x * FLAG_CHUNK + threadIdx.x * 16ull;
+    uint32_t c = 0;
+    for (uint32_t k = 0; k < 16; ++k)
+        if (base + k < len) c += buf[base + k] == FLAG;
+    __shared__ uint32_t s;
+    if (threadIdx.x == 0) s = 0;
+    __syncthreads();
+    atomicAdd(&s, c);
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void k_flag_scatter(const uint8_t *buf, uint64_t len, const uint64_t *cnt_off,
+                                                      uint64_t *pos) {
+    const uint64_t base = (uint64_t)blockIdx.x * FLAG_CHUNK + threadIdx.x * 16ull;
+    uint32_t c = 0;
+    for (uint32_t k = 0; k < 16; ++k)
+        if (base + k < len) c += buf[base + k] == FLAG;
+    // in-order rank of this thread's flags inside the chunk
+    __shared__ uint32_t sh[256];
+    sh[threadIdx.x] = c;
+    __syncthreads();
+    for (uint32_t d = 1; d < 256; d <<= 1) {
+        const uint32_t add = threadIdx.x >= d ? sh[threadIdx.x - d] : 0;
+        __syncthreads();
+        sh[threadIdx.x] += add;
+        __syncthreads();
+    }
+    uint64_t w = cnt_off[blockIdx.x] + sh[threadIdx.x] - c;
+    for (uint32_t k = 0; k < 16; ++k)
+        if (base + k < len && buf[base + k] == FLAG) pos[w++] = base + k;
+}
+
+// One lane per consecutive flag pair (k, k+1): the read loop's frame
+// buf[pos_k+1 : pos_{k+1}) with its two bytes.replace passes (TCPInterface.py:
+// 397-398: ESC,5E -> 7E first, then ESC,5D -> 7D, each left to right and
+// non-overlapping), written at out + pos_k + 1.
+__global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, const uint64_t *pos, const uint64_t *nflags_p,
+                                                       uint64_t max_pairs, uint32_t hw_mtu, uint32_t ifac_size,
+                                                       uint8_t *out, uint64_t *frame_off, uint32_t *frame_len,
+                                                       int32_t *status) {
+    const uint64_t nf = *nflags_p;
+    uint64_t npairs = nf > 1 ? nf - 1 : 0;
+    if (npairs > max_pairs) npairs = max_pairs;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < npairs;
+         k += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t a = pos[k] + 1, e = pos[k + 1];
+        uint8_t *o = out + a;
+        uint64_t w = 0;
+        for (uint64_t r = a; r < e;) {                     // pass 1
+            if (buf[r] == ESC && r + 1 < e && buf[r + 1] == (FLAG ^ ESC_MASK)) {
+                o[w++] = FLAG;
+                r += 2;
+            } else {
+                o[w++] = buf[r++];
+            }
+        }
+        const uint64_t n1 = w;
+        w = 0;
+        for (uint64_t r = 0; r < n1;) {                    // pass 2, in place (w <= r)
+            if (o[r] == ESC && r + 1 < n1 && o[r + 1] == (ESC ^ ESC_MASK)) {
+                o[w++] = ESC;
+                r += 2;
+            } else {
+                o[w++] = o[r++];
+            }
+        }
+        frame_off[k] = a;
+        frame_len[k] = (uint32_t)w;
+        // check_frame_len (TCPInterface.py:336-339); empty frames are skipped (:400)
+        status[k] = w == 0 ? RT_FRAME_EMPTY
+                           : ((w <= HEADER_MINSIZE || w > (uint64_t)hw_mtu + ifac_size) ? RT_FRAME_BAD_LEN
+                                                                                        : RT_FRAME_OK);
+    }
+}
+
+__global__ void k_deframe_counts(const uint64_t *nflags_p, const uint64_t *pos, uint64_t len, uint32_t hw_mtu,
+                                 uint64_t *counts) {
+    const uint64_t nf = *nflags_p;
+    counts[0] = nf > 1 ? nf - 1 : 0;
+    // what the loop keeps: from the last flag on, unless it is more than 2*HW_MTU
+    // long (:406-407); with no flag at all the buffer is dropped (:408-410)
+    uint64_t consumed = len;
+    if (nf > 0) {
+        const uint64_t last = pos[nf - 1];
+        consumed = (len - last > 2ull * hw_mtu) ? len : last;
+    }
+    counts[1] = consumed;
+}
+
+// ------------------------------------------------------------------ IFAC --
+
+// HMAC midstates for a <= 64-byte key given as bytes
+__device__ __forceinline__ void key_midstates(const uint8_t *key, uint32_t klen, uint32_t hi[8], uint32_t ho[8]) {
+    uint32_t wi[16], wo[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t q = 4u * k + j;
+            v = (v << 8) | (q < klen ? key[q] : 0u);
+        }
+        wi[k] = v ^ 0x36363636u;
+        wo[k] = v ^ 0x5c5c5c5cu;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) hi[k] = ho[k] = SHA_IV[k];
+    sha256_compress(hi, wi);
+    sha256_compress(ho, wo);
+}
+
+// One lane per packet.  Outbound (MASK): new_raw = [raw0|0x80, raw1] || ifac ||
+// raw[2:], masked with HKDF(len+ifac_size, ifac, ifac_key) except the IFAC
+// bytes, byte 0 keeps the flag (Transport.py:1069-1101).  Inbound: the IFAC
+// is raw[2:2+n], mask = HKDF(len, ifac, ifac_key) over everything but the
+// IFAC, reassembled [un0 & 0x7f, un1] || un[2+n:] (Transport.py:1441-1475).
+template <bool MASK>
+__global__ __launch_bounds__(256) void k_ifac(IfacArgs a) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const uint8_t *raw = a.pkt + a.pkt_off[i];
+    const uint32_t L = a.pkt_len[i], n = a.ifac_size;
+    uint8_t *o = a.out + a.out_off[i];
+    const uint8_t *ifac;
+    if (MASK) {
+        ifac = a.ifac + (uint64_t)i * n;
+    } else {
+        // len(raw) > 2, IFAC flag set, len(raw) > 2 + ifac_size (:1441-1445)
+        const bool ok = L > 2u && (raw[0] & 0x80u) && L > 2u + n;
+        a.status[i] = ok ? 0 : 1;
+        if (!ok) return;
+        ifac = raw + 2;
+        for (uint32_t k = 0; k < n; ++k) a.ifac[(uint64_t)i * n + k] = ifac[k];
+    }
+    const uint32_t total = MASK ? L + n : L;           // HKDF output length
+    // HKDF (HKDF.py:35-62) with salt = ifac_key, ikm = ifac, no context:
+    // PRK = HMAC(ifac_key, ifac); T_b = HMAC(PRK, T_{b-1} || b+1)
+    uint32_t hi[8], ho[8], prk[8];
+    key_midstates(a.ifac_key, a.key_len, hi, ho);
+    {
+        uint32_t w[16], h[8];
+        // ifac_size <= 64: one or two message blocks after the ipad block
+        const uint64_t bits = (64ull + n) * 8ull;
+        const uint32_t nblk = (n + 8u) / 64u + 1u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) h[k] = hi[k];
+        for (uint32_t b = 0; b < nblk; ++b) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t q = 64u * b + 4u * k + j;
+                    v = (v << 8) | (q < n ? ifac[q] : (q == n ? 0x80u : 0u));
+                }
+                w[k] = v;
+            }
+            if (b + 1 == nblk) {
+                w[14] = (uint32_t)(bits >> 32);
+                w[15] = (uint32_t)bits;
+            }
+            sha256_compress(h, w);
+        }
+        hmac_outer(prk, h, ho);
+    }
+    uint8_t prkb[32];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        prkb[4 * k] = prk[k] >> 24; prkb[4 * k + 1] = prk[k] >> 16; prkb[4 * k + 2] = prk[k] >> 8; prkb[4 * k + 3] = prk[k];
+    }
+    uint32_t phi[8], pho[8];
+    key_midstates(prkb, 32, phi, pho);
+    uint32_t t[8];
+    uint64_t w_out = 0;                                   // inbound: write position in the reassembled packet
+    for (uint32_t b = 0; 32u * b < total; ++b) {
+        // message T_{b-1} (32 B, none for b = 0) || counter byte
+        uint32_t w[16], h[8];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = 0;
+        if (b == 0) {
+            w[0] = ((b + 1u) & 255u) << 24 | 0x800000u;
+            w[15] = (64u + 1u) * 8u;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) w[k] = t[k];
+            w[8] = ((b + 1u) & 255u) << 24 | 0x800000u;
+            w[15] = (64u + 33u) * 8u;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) h[k] = phi[k];
+        sha256_compress(h, w);
+        hmac_outer(t, h, pho);
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const uint32_t pos = 32u * b + j;
+            if (pos >= total) continue;
+            const uint8_t m = (uint8_t)(t[j >> 2] >> (24 - 8 * (j & 3)));
+            if (MASK) {
+                uint8_t v;
+                if (pos == 0) v = (uint8_t)(((raw[0] | 0x80u) ^ m) | 0x80u);
+                else if (pos == 1) v = raw[1] ^ m;
+                else if (pos < 2u + n) v = ifac[pos - 2];                 // the IFAC itself is not masked
+                else v = raw[pos - n] ^ m;
+                o[pos] = v;
+            } else {
+                if (pos == 0) o[w_out++] = (uint8_t)((raw[0] ^ m) & 0x7Fu);
+                else if (pos == 1) o[w_out++] = raw[1] ^ m;
+                else if (pos >= 2u + n) o[w_out++] = raw[pos] ^ m;
+            }
+        }
+    }
+}
+
+// --------------------------------------------------------- packet header --
+
+// SHA-256 over  first || src[0..len)  (one modified leading byte, then bytes)
+__device__ void sha_prefixed(uint8_t first, const uint8_t *src, uint32_t len, uint32_t out[8]) {
+    uint32_t h[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = SHA_IV[k];
+    const uint32_t m = len + 1u;
+    const uint64_t bits = (uint64_t)m * 8u;
+    const uint32_t nblk = (m + 8u) / 64u + 1u;
+    for (uint32_t b = 0; b < nblk; ++b) {
+        uint32_t w[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t q = 64u * b + 4u * k + j;
+                const uint32_t byte = q == 0 ? first : (q < m ? src[q - 1] : (q == m ? 0x80u : 0u));
+                v = (v << 8) | byte;
+            }
+            w[k] = v;
+        }
+        if (b + 1 == nblk) {
+            w[14] = (uint32_t)(bits >> 32);
+            w[15] = (uint32_t)bits;
+        }
+        sha256_compress(h, w);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out[k] = h[k];
+}
+
+__global__ __launch_bounds__(256) void k_unpack(const uint8_t *pkt, const uint64_t *off, const uint32_t *len,
+                                                rt_packet_fields *out, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t *raw = pkt + off[i];
+    const uint32_t L = len[i];
+    rt_packet_fields f;
+    __builtin_memset(&f, 0, sizeof(f));
+    if (L >= 2) {
+        f.flags = raw[0];
+        f.hops = raw[1];
+        f.header_type = (f.flags >> 6) & 1u;
+        f.context_flag = (f.flags >> 5) & 1u;
+        f.transport_type = (f.flags >> 4) & 1u;
+        f.destination_type = (f.flags >> 2) & 3u;
+        f.packet_type = f.flags & 3u;
+        const uint32_t ctx_at = f.header_type ? 2u * DST_LEN + 2u : DST_LEN + 2u;
+        // hops < PATHFINDER_M (Packet.py:242-243); ord() of the context byte needs it present
+        if (f.hops < PATHFINDER_M && L > ctx_at) {
+            f.ok = 1;
+            f.context = raw[ctx_at];
+            f.data_offset = ctx_at + 1u;
+            f.data_len = L - f.data_offset;
+            const uint8_t *dst = raw + (f.header_type ? 2u + DST_LEN : 2u);
+            for (int k = 0; k < 16; ++k) f.destination_hash[k] = dst[k];
+            if (f.header_type)
+                for (int k = 0; k < 16; ++k) f.transport_id[k] = raw[2 + k];
+            // get_hashable_part: flags & 0x0F || raw[2:] (header 1) or raw[18:] (header 2)
+            const uint32_t from = f.header_type ? DST_LEN + 2u : 2u;
+            uint32_t d[8];
+            sha_prefixed(f.flags & 0x0Fu, raw + from, L - from, d);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                f.packet_hash[4 * k] = d[k] >> 24; f.packet_hash[4 * k + 1] = d[k] >> 16;
+                f.packet_hash[4 * k + 2] = d[k] >> 8; f.packet_hash[4 * k + 3] = d[k];
+            }
+        }
+    }
+    out[i] = f;
+}
+
+__global__ __launch_bounds__(256) void k_pack_headers(PackArgs a) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    uint8_t *o = a.out + a.out_off[i];
+    o[0] = a.flags[i];
+    o[1] = a.hops ? a.hops[i] : 0;
+    uint32_t w = 2;
+    if (a.transport_id) {
+        for (int k = 0; k < 16; ++k) o[w + k] = a.transport_id[16ull * i + k];
+        w += 16;
+    }
+    for (int k = 0; k < 16; ++k) o[w + k] = a.destination_hash[16ull * i + k];
+    o[w + 16] = a.context[i];
+}
+
+}  // namespace
+
+// ------------------------------------------------------------- launchers --
+
+uint64_t scan_workspace_bytes(uint64_t n) { return 8ull * ((n + SCAN_BLOCK - 1) / SCAN_BLOCK + 1); }
+
+// out[i] = sum(in[0..i)); *total (device) = sum(in)
+static hipError_t launch_scan(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *part, uint64_t *total,
+                              hipStream_t s) {
+    const uint64_t nb = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scan_block, dim3((unsigned)nb), dim3(SCAN_BLOCK), 0, s, in, out, part, n);
+    hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(SCAN_BLOCK), 0, s, part, nb);
+    hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(SCAN_BLOCK), 0, s, out, part, n, total);
+    return hipGetLastError();
+}
+
+uint64_t hdlc_frame_workspace_bytes(uint32_t n) { return 8ull * n + scan_workspace_bytes(n) + 64; }
+
+hipError_t launch_hdlc_frame(const uint8_t *pkt, const uint64_t *off, const uint32_t *len, uint32_t n, uint8_t *out,
+                             uint64_t *frame_off, void *ws, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    uint64_t *flen = (uint64_t *)ws;
+    uint64_t *part = flen + n;
+    const unsigned g = (n + 255) / 256;
+    hipLaunchKernelGGL(k_hdlc_count, dim3(g), dim3(256), 0, s, pkt, off, len, flen, n);
+    hipError_t e = launch_scan(flen, frame_off, n, part, frame_off + n, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_hdlc_write, dim3(g), dim3(256), 0, s, pkt, off, len, frame_off, out, n);
+    return hipGetLastError();
+}
+
+uint64_t hdlc_deframe_workspace_bytes(uint64_t len) {
+    const uint64_t chunks = (len + FLAG_CHUNK - 1) / FLAG_CHUNK;
+    return 8ull * chunks * 2 + scan_workspace_bytes(chunks) + 8ull * (len + 1) + 64;
+}
+
+hipError_t launch_hdlc_deframe(const uint8_t *buf, uint64_t len, uint32_t hw_mtu, uint32_t ifac_size, uint8_t *out,
+                               uint64_t *frame_off, uint32_t *frame_len, int32_t *status, uint64_t *counts,
+                               uint64_t max_pairs, void *ws, hipStream_t s) {
+    const uint64_t chunks = (len + FLAG_CHUNK - 1) / FLAG_CHUNK;
+    uint64_t *cnt = (uint64_t *)ws;
+    uint64_t *cnt_off = cnt + chunks;
+    uint64_t *part = cnt_off + chunks;
+    uint64_t *nflags = part + (chunks + SCAN_BLOCK - 1) / SCAN_BLOCK + 1;
+    uint64_t *pos = nflags + 1;
+    hipError_t e = hipMemsetAsync(nflags, 0, 8, s);
+    if (e != hipSuccess) return e;
+    if (chunks) {
+        hipLaunchKernelGGL(k_flag_count, dim3((unsigned)chunks), dim3(256), 0, s, buf, len, cnt);
+        if ((e = launch_scan(cnt, cnt_off, chunks, part, nflags, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_flag_scatter, dim3((unsigned)chunks), dim3(256), 0, s, buf, len, cnt_off, pos);
+    }
+    hipLaunchKernelGGL(k_deframe_counts, dim3(1), dim3(1), 0, s, nflags, pos, len, hw_mtu, counts);
+    // the pair count lives on the device: a grid-stride kernel sized by the caller's capacity
+    if (max_pairs) {
+        uint64_t g = (max_pairs + 255) / 256;
+        if (g > 4096) g = 4096;
+        hipLaunchKernelGGL(k_hdlc_unescape, dim3((unsigned)g), dim3(256), 0, s, buf, pos, nflags, max_pairs, hw_mtu,
+                           ifac_size, out, frame_off, frame_len, status);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_ifac(const IfacArgs &a, bool mask, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    const unsigned g = (a.n + 255) / 256;
+    if (mask)
+        hipLaunchKernelGGL(k_ifac<true>, dim3(g), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_ifac<false>, dim3(g), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack(const uint8_t *pkt, const uint64_t *off, const uint32_t *len, void *fields, uint32_t n,
+                         hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_unpack, dim3((n + 255) / 256), dim3(256), 0, s, pkt, off, len, (rt_packet_fields *)fields, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_headers(const PackArgs &a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pack_headers, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace rnstok

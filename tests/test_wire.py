@@ -1,0 +1,188 @@
+"""Wire-side neighbours: HDLC framing / deframing
+(TCPInterface.py:44-53, 323, 387-410), IFAC mask / unmask (Transport.py:
+1069-1101, 1441-1475), Packet unpack / hash / header pack (Packet.py:
+167-268, 342-353).
+
+CPU: the oracle (oracle/wire.py) against fixtures produced by the
+reference's own code (tests/golden/gen_wire.py: HDLC.escape, the real
+TCPClientInterface.read_loop over a fake socket, Transport.transmit /
+inbound with a real Ed25519 identity, Packet.unpack / pack).
+GPU (-m gpu): the wire kernels through the C-ABI, bit-exact against the same
+fixtures and against the oracle on random batches.
+"""
+import importlib.util
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import wire as ow
+from tests_helpers import b
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def wv():
+    with open(os.path.join(HERE, "golden", "wire_vectors.json")) as f:
+        return json.load(f)
+
+
+def _oversized_body():
+    spec = importlib.util.spec_from_file_location("gen_wire", os.path.join(HERE, "golden", "gen_wire.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    return g.oversized_body()
+
+
+def _stream(r):
+    return b(r["stream"]) if r["stream"] is not None else b"\x7e" + _oversized_body() + b(r["stream_tail"])
+
+
+def _h(x):
+    return None if x is None else b(x)
+
+
+# ------------------------------------------------------------------ oracle --
+
+def test_oracle_escape(wv):
+    for e in wv["escape"]:
+        assert ow.hdlc_escape(b(e["data"])).hex() == e["escaped"]
+
+
+def test_oracle_deframe_matches_reference_read_loop(wv):
+    for r in wv["deframe"]:
+        frames, invalid, _ = ow.deframe(_stream(r), r["hw_mtu"], r["ifac_size"])
+        assert [f.hex() for f in frames] == r["frames"], r["name"]
+        assert invalid == r["invalid"], r["name"]
+    c = wv["deframe_chunked"]
+    buf, got = b"", []
+    for ch in c["chunks"]:
+        fr, _, buf = ow.deframe(buf + b(ch))
+        got += fr
+    assert [f.hex() for f in got] == c["frames"]
+
+
+def test_oracle_ifac(wv):
+    for r in wv["ifac"]:
+        m = ow.ifac_mask(b(r["raw"]), b(r["ifac"]), b(r["ifac_key"]))
+        assert m.hex() == r["masked"]
+        ifac, new_raw = ow.ifac_unmask(m, r["ifac_size"], b(r["ifac_key"]))
+        assert ifac.hex() == r["ifac"] and new_raw.hex() == r["inbound_reassembled"] == r["raw"]
+
+
+def test_oracle_unpack_and_pack(wv):
+    for r in wv["unpack"]:
+        u = ow.unpack(b(r["raw"]))
+        assert (u is not None) == r["ok"], r["raw"][:8]
+        if u:
+            for k in ("header_type", "context_flag", "transport_type", "destination_type", "packet_type", "hops",
+                      "flags", "context"):
+                assert u[k] == r[k], k
+            assert u["data"].hex() == r["data"] and u["packet_hash"].hex() == r["packet_hash"]
+            assert u["destination_hash"].hex() == r["destination_hash"]
+            assert (None if u["transport_id"] is None else u["transport_id"].hex()) == r["transport_id"]
+    for r in wv["pack"]:
+        h = ow.pack_header(r["flags"], r["hops"], b(r["destination_hash"]), r["context"], _h(r["transport_id"]))
+        assert (h + b(r["data"])).hex() == r["raw"]
+        assert ow.unpack(b(r["raw"]))["packet_hash"].hex() == r["packet_hash"]
+
+
+# --------------------------------------------------------------------- GPU --
+
+@pytest.mark.gpu
+def test_gpu_escape_and_frame(wv):
+    from reticulum_amd import wire
+    for e in wv["escape"]:
+        assert wire.HDLC.escape(b(e["data"])).hex() == e["escaped"]
+    rng = np.random.Generator(np.random.PCG64(323))
+    pk = []
+    for n in rng.integers(0, 700, 2000):
+        a = rng.integers(0, 256, int(n), dtype=np.uint8)
+        a[rng.random(int(n)) < 0.1] = 0x7E
+        a[rng.random(int(n)) < 0.1] = 0x7D
+        pk.append(a.tobytes())
+    stream, off = wire.hdlc_frame_batch(pk)
+    assert stream == b"".join(ow.hdlc_frame(p) for p in pk)
+    assert all(stream[int(off[i]):int(off[i + 1])] == ow.hdlc_frame(p) for i, p in enumerate(pk[:50]))
+
+
+@pytest.mark.gpu
+def test_gpu_deframe_matches_reference_read_loop(wv):
+    from reticulum_amd import wire
+    for r in wv["deframe"]:
+        frames, invalid, consumed = wire.deframe(_stream(r), r["hw_mtu"], r["ifac_size"] or 0)
+        assert [f.hex() for f in frames] == r["frames"], r["name"]
+        assert invalid == r["invalid"], r["name"]
+        _, _, rest = ow.deframe(_stream(r), r["hw_mtu"], r["ifac_size"])
+        assert _stream(r)[consumed:] == rest, r["name"]
+    c = wv["deframe_chunked"]
+    d = wire.Deframer()
+    got = []
+    for ch in c["chunks"]:
+        got += d.feed(b(ch))
+    assert [f.hex() for f in got] == c["frames"]
+
+
+@pytest.mark.gpu
+def test_gpu_frame_deframe_roundtrip_large():
+    """Size-independent property: 20 000 framed packets deframe to themselves."""
+    from reticulum_amd import wire
+    rng = np.random.Generator(np.random.PCG64(410))
+    pk = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(20, 520, 20000)]
+    stream, _ = wire.hdlc_frame_batch(pk)
+    frames, invalid, consumed = wire.deframe(stream)
+    assert frames == pk and invalid == [] and consumed == len(stream) - 1
+
+
+@pytest.mark.gpu
+def test_gpu_ifac(wv):
+    from reticulum_amd import wire
+    for size in (8, 16):
+        rs = [r for r in wv["ifac"] if r["ifac_size"] == size]
+        key = b(rs[0]["ifac_key"])
+        masked = wire.ifac_mask_batch([b(r["raw"]) for r in rs], [b(r["ifac"]) for r in rs], key)
+        assert [m.hex() for m in masked] == [r["masked"] for r in rs]
+        un = wire.ifac_unmask_batch(masked, size, key)
+        assert [(i.hex(), p.hex()) for i, p in un] == [(r["ifac"], r["inbound_reassembled"]) for r in rs]
+    # random batch vs the oracle, with packets the reference drops before signing
+    rng = np.random.Generator(np.random.PCG64(1101))
+    key = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+    raws = [rng.integers(0, 128, 2, dtype=np.uint8).tobytes() + rng.integers(0, 256, int(n), dtype=np.uint8).tobytes()
+            for n in rng.integers(0, 600, 500)]
+    ifacs = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in raws]
+    masked = wire.ifac_mask_batch(raws, ifacs, key)
+    assert masked == [ow.ifac_mask(r, f, key) for r, f in zip(raws, ifacs)]
+    probes = masked + [bytes([0x05]) + m[1:] for m in masked[:20]] + [m[:18] for m in masked[:20]] + [b"\x80\x01"]
+    got = wire.ifac_unmask_batch(probes, 16, key)
+    assert got == [ow.ifac_unmask(p, 16, key) for p in probes]
+
+
+@pytest.mark.gpu
+def test_gpu_unpack_and_pack(wv):
+    from reticulum_amd import wire
+    raws = [b(r["raw"]) for r in wv["unpack"]]
+    got = wire.unpack_batch(raws)
+    for r, g in zip(wv["unpack"], got):
+        assert (g is not None) == r["ok"], r["raw"][:8]
+        if g:
+            assert g["packet_hash"].hex() == r["packet_hash"] and g["data"].hex() == r["data"]
+            assert g["destination_hash"].hex() == r["destination_hash"] and g["context"] == r["context"]
+            assert (None if g["transport_id"] is None else g["transport_id"].hex()) == r["transport_id"]
+            for k in ("header_type", "context_flag", "transport_type", "destination_type", "packet_type", "hops"):
+                assert g[k] == r[k], k
+    for ht in (0, 1):
+        rs = [r for r in wv["pack"] if (r["transport_id"] is not None) == bool(ht)]
+        hdrs = wire.pack_headers_batch([r["flags"] for r in rs], [r["hops"] for r in rs],
+                                       [b(r["destination_hash"]) for r in rs], [r["context"] for r in rs],
+                                       [b(r["transport_id"]) for r in rs] if ht else None)
+        assert [(h + b(r["data"])).hex() for h, r in zip(hdrs, rs)] == [r["raw"] for r in rs]
+    rng = np.random.Generator(np.random.PCG64(268))
+    raws = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(0, 520, 3000)]
+    got = wire.unpack_batch(raws)
+    for raw, g in zip(raws, got):
+        o = ow.unpack(raw)
+        assert (g is None) == (o is None)
+        if g:
+            assert g == {k: o[k] for k in g}

@@ -254,6 +254,44 @@ __device__ __forceinline__ void hmac_outer(uint32_t tag[8], const uint32_t inner
     sha256_compress(tag, w);
 }
 
+// The last compressions of an HMAC through ONE inlined sha256_compress, so a
+// kernel's packet loop carries a single copy of the 64 unrolled rounds:
+// k = first..2 runs the full block `blk` (k = 0), the final padded block `fin`
+// (k = 1) and the outer hash of the inner digest under the opad midstate
+// (k = 2).  h: the inner state in, the tag out.
+__device__ __forceinline__ void hmac_finish(uint32_t h[8], uint32_t first, const uint32_t blk[16],
+                                            const uint32_t fin[16], const uint32_t opad[8]) {
+#pragma nounroll
+    for (uint32_t k = first; k < 3u; ++k) {
+        uint32_t w[16];
+        if (k == 2u) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                w[j] = h[j];
+                h[j] = opad[j];
+            }
+            w[8] = 0x80000000u;
+#pragma unroll
+            for (int j = 9; j < 15; ++j) w[j] = 0u;
+            w[15] = (64u + 32u) * 8u;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) w[j] = k == 0u ? blk[j] : fin[j];
+        }
+        sha256_compress(h, w);
+    }
+}
+
+// Final padded block of an HMAC inner hash: the first fu (0..3) 16-B units of
+// u (big-endian words), 0x80, zeros, the 64-bit message length in bits.
+__device__ __forceinline__ void sha_final_block(uint32_t fin[16], const uint32_t u[16], uint32_t fu, uint64_t bits) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        fin[k] = (uint32_t)k < 4u * fu ? u[k] : ((uint32_t)k == 4u * fu ? 0x80000000u : 0u);
+    fin[14] = (uint32_t)(bits >> 32);
+    fin[15] = (uint32_t)bits;
+}
+
 // Generic byte-granular HMAC inner hash (rare lanes: malformed token lengths).
 // Hashes n bytes at p after the 64-byte ipad block.
 __device__ __noinline__ void sha_bytes_after_ipad(uint32_t h[8], const uint8_t *p, uint64_t n) {

@@ -181,68 +181,65 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
         uint32_t h[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) h[i] = ipad[i];
-        // Software pipeline: the SHA-256 compression of quad q-1's units is
-        // interleaved round by round with quad q's AES chain (enc_quad), so
-        // every wave carries an LDS-latency-bound and a VALU-bound chain.
-        u32x4 prev = iv;
-        Sha256 S;                       // S.w: pending SHA block (previous quad's units)
-        u32x4 x[4], c[4];
-        if (nq > 0) {
-            x[0] = ld16(P); x[1] = ld16(P + 16); x[2] = ld16(P + 32); x[3] = ld16(P + 48);
-            enc_quad<NR, false>(c, x, prev, K.rk, LN, S);
-            st16(C, c[0]); st16(C + 16, c[1]); st16(C + 32, c[2]); st16(C + 48, c[3]);
-            sha_units(S.w, prev, c[0], c[1], c[2]);
-            prev = c[3];
-            P += 64; C += 64;
-        }
-        for (uint32_t q = 1; q < nq; ++q) {
-            x[0] = ld16(P); x[1] = ld16(P + 16); x[2] = ld16(P + 32); x[3] = ld16(P + 48);
-            S.start(h);
-            enc_quad<NR, true>(c, x, prev, K.rk, LN, S);
-            S.finish(h);
-            st16(C, c[0]); st16(C + 16, c[1]); st16(C + 32, c[2]); st16(C + 48, c[3]);
-            sha_units(S.w, prev, c[0], c[1], c[2]);
-            prev = c[3];
-            P += 64; C += 64;
-        }
-        // tail: tb (1..4) blocks, the last one carries the PKCS7 pad; all four
-        // slots are computed (unused ones on zeros, never stored) so the
-        // pending compression can ride on the tail's AES chain.
+        // One enc_quad instance serves every quad, the tail quad (tb blocks,
+        // the last one carrying the PKCS7 pad; unused slots run on zeros and
+        // are not stored) included; the SHA-256 compression of quad q-1's
+        // units rides on quad q's AES chain (quad 0's SHA slot hashes zeros
+        // and is dropped).  hmac_finish runs the last 2-3 compressions through
+        // one sha256_compress: one copy of each, 49 KB of code where a
+        // head/body/tail-specialised loop took 150 KB (same speed on c2,
+        // measured; 2-7 % faster with per-packet keys).
         {
             const u32x4 z = {0u, 0u, 0u, 0u};
-            const uint32_t r = L & 15u;
+            const uint32_t rem = L & 15u;
+            u32x4 prev = iv, x[4], c[4];
+            Sha256 S;                       // S.w: the pending SHA block (previous quad's units)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                x[j] = (uint32_t)j + 1u < tb ? ld16(P + 16 * j) : ((uint32_t)j + 1u == tb ? pad_block(P + 16 * j, r) : z);
+            for (int k = 0; k < 16; ++k) S.w[k] = 0u;
+#pragma nounroll
+            for (uint32_t q = 0; q <= nq; ++q) {
+                if (q < nq) {
+                    x[0] = ld16(P); x[1] = ld16(P + 16); x[2] = ld16(P + 32); x[3] = ld16(P + 48);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        x[j] = (uint32_t)j + 1u < tb ? ld16(P + 16 * j)
+                                                     : ((uint32_t)j + 1u == tb ? pad_block(P + 16 * j, rem) : z);
+                }
+                S.start(h);
+                enc_quad<NR, true>(c, x, prev, K.rk, LN, S);
+                // The SHA rounds' results are consumed here, in the AES
+                // chain's block: otherwise the compiler sinks the rounds
+                // past the stores below and the two chains run back to back.
+                // (A select, not a branch, for quad 0's dropped compression.)
+#pragma unroll
+                for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(S.v[k]));
+                const bool keep = q > 0u;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) h[k] += keep ? S.v[k] : 0u;
+                const uint32_t nst = q < nq ? 4u : tb;
+                st16(C, c[0]);
+                if (nst > 1u) st16(C + 16, c[1]);
+                if (nst > 2u) st16(C + 32, c[2]);
+                if (nst > 3u) st16(C + 48, c[3]);
+                sha_units(S.w, prev, c[0], c[1], c[2]);
+                prev = c[3];
+                P += 64; C += 64;
+            }
+            // S.w: units u0..u3 of the tail quad (u0 = the block before it),
+            // prev = u4; tu = tb + 1 units are left for the inner hash: a full
+            // block u0..u3 when tu >= 4, then the final padded block.
+            const uint32_t tu = tb + 1u;
+            uint32_t u4[16], fin[16];
+            sha_units(u4, prev, z, z, z);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) u4[k] = tu >= 4u ? u4[k] : S.w[k];
+            sha_final_block(fin, u4, tu >= 4u ? tu - 4u : tu, (uint64_t)(64u + 16u + 16u * (nfull + 1u)) * 8u);
+            hmac_finish(h, tu >= 4u ? 0u : 1u, S.w, fin, opad);
+            uint8_t *T = O + 16 + 16ull * (nfull + 1u);
+            st16(T, u32x4{bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3])});
+            st16(T + 16, u32x4{bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7])});
         }
-        if (nq > 0) {
-            S.start(h);
-            enc_quad<NR, true>(c, x, prev, K.rk, LN, S);
-            S.finish(h);
-        } else {
-            enc_quad<NR, false>(c, x, prev, K.rk, LN, S);
-        }
-        st16(C, c[0]);
-        if (tb > 1) st16(C + 16, c[1]);
-        if (tb > 2) st16(C + 32, c[2]);
-        if (tb > 3) st16(C + 48, c[3]);
-        const u32x4 u0 = prev, u1 = c[0], u2 = c[1], u3 = c[2], u4 = c[3];
-        const uint32_t tu = tb + 1;   // units left for the SHA tail (2..5)
-        const uint64_t bits = (uint64_t)(64u + 16u + 16u * (nfull + 1u)) * 8u;
-        if (tu >= 4) {
-            uint32_t w[16];
-            sha_units(w, u0, u1, u2, u3);
-            sha256_compress(h, w);
-            sha_final_units(h, tu - 4, u4, u4, u4, bits);
-        } else {
-            sha_final_units(h, tu, u0, u1, u2, bits);
-        }
-        uint32_t tag[8];
-        hmac_outer(tag, h, opad);
-        u32x4 t0 = {bswap(tag[0]), bswap(tag[1]), bswap(tag[2]), bswap(tag[3])};
-        u32x4 t1 = {bswap(tag[4]), bswap(tag[5]), bswap(tag[6]), bswap(tag[7])};
-        st16(C + 16 * tb, t0);
-        st16(C + 16 * tb + 16, t1);
     }
 }
 
@@ -441,63 +438,60 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_DEC : WG_DEC) void k_decr
             uint32_t h[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) h[i] = ipad[i];
+            // One dec_quad instance serves every quad, the tail quad (tb
+            // blocks) included; its SHA slot hashes the same quad's units
+            // (dropped for a tail of tb < 3, whose units are not a full
+            // block).  hmac_finish runs the final block and the outer hash
+            // through one sha256_compress.
+            const u32x4 z = {0u, 0u, 0u, 0u};
             u32x4 prev = ld16(Kt);
             const uint8_t *C = Kt + 16;
             uint8_t *D = O;
             Sha256 S;
             u32x4 c[4], pp[4];
-            for (uint32_t q = 0; q < nq; ++q) {
-                c[0] = ld16(C); c[1] = ld16(C + 16); c[2] = ld16(C + 32); c[3] = ld16(C + 48);
+#pragma nounroll
+            for (uint32_t q = 0; q <= nq; ++q) {
+                const uint32_t nbk = q < nq ? 4u : tb;
+                c[0] = ld16(C);
+                c[1] = nbk > 1u ? ld16(C + 16) : z;
+                c[2] = nbk > 2u ? ld16(C + 32) : z;
+                c[3] = nbk > 3u ? ld16(C + 48) : z;
                 S.start(h);
                 sha_units(S.w, prev, c[0], c[1], c[2]);
                 dec_quad<NR, true>(pp, c, prev, K.rk, LN, S);
-                S.finish(h);
-                st16(D, pp[0]); st16(D + 16, pp[1]); st16(D + 32, pp[2]); st16(D + 48, pp[3]);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(S.v[k]));   // see k_encrypt
+                const bool keep = nbk >= 3u;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) h[k] += keep ? S.v[k] : 0u;
+                st16(D, pp[0]);
+                if (nbk > 1u) st16(D + 16, pp[1]);
+                if (nbk > 2u) st16(D + 32, pp[2]);
+                if (nbk > 3u) st16(D + 48, pp[3]);
                 prev = c[3];
                 C += 64; D += 64;
             }
-            // tail: tb (1..4) blocks; when tb >= 3 the units prev,c0,c1,c2 form a
-            // full SHA block, compressed inside the tail's AES chain.
-            {
-                const u32x4 z = {0u, 0u, 0u, 0u};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) c[j] = (uint32_t)j < tb ? ld16(C + 16 * j) : z;
-            }
-            const bool full = tb >= 3;
-            if (full) {
-                S.start(h);
-                sha_units(S.w, prev, c[0], c[1], c[2]);
-                dec_quad<NR, true>(pp, c, prev, K.rk, LN, S);
-                S.finish(h);
-            } else {
-                dec_quad<NR, false>(pp, c, prev, K.rk, LN, S);
-            }
-            st16(D, pp[0]);
-            if (tb > 1) st16(D + 16, pp[1]);
-            if (tb > 2) st16(D + 32, pp[2]);
-            if (tb > 3) st16(D + 48, pp[3]);
-            const u32x4 last = tb == 1 ? pp[0] : (tb == 2 ? pp[1] : (tb == 3 ? pp[2] : pp[3]));
-            const u32x4 u0 = prev, u1 = c[0], u2 = c[1], u4 = c[3];
-            const uint32_t tu = tb + 1;
-            const uint64_t bits = (uint64_t)(64u + 16u + 16u * nb) * 8u;
-            if (full)
-                sha_final_units(h, tu - 4, u4, u4, u4, bits);
-            else
-                sha_final_units(h, tu, u0, u1, u2, bits);
-            uint32_t tag[8];
-            hmac_outer(tag, h, opad);
-            const u32x4 r0 = ld16(C + 16 * tb), r1 = ld16(C + 16 * tb + 16);
-            const uint32_t diff = (r0.x ^ bswap(tag[0])) | (r0.y ^ bswap(tag[1])) | (r0.z ^ bswap(tag[2])) |
-                                  (r0.w ^ bswap(tag[3])) | (r1.x ^ bswap(tag[4])) | (r1.y ^ bswap(tag[5])) |
-                                  (r1.z ^ bswap(tag[6])) | (r1.w ^ bswap(tag[7]));
+            // the tail quad: pb = the block before it (re-read rather than
+            // kept live through the loop), c[0..tb-1] its ciphertext,
+            // pp[0..tb-1] its plaintext
+            const u32x4 pb = ld16(Kt + 64ull * nq);
+            const u32x4 r0 = ld16(Kt + (T - 32u)), r1 = ld16(Kt + (T - 16u));
+            const u32x4 last = tb == 1u ? pp[0] : (tb == 2u ? pp[1] : (tb == 3u ? pp[2] : pp[3]));
+            const bool full = tb >= 3u;
+            const uint32_t tu = tb + 1u;
+            uint32_t u[16], fin[16];
+            sha_units(u, full ? c[3] : pb, c[0], c[1], z);
+            sha_final_block(fin, u, full ? tu - 4u : tu, (uint64_t)(64u + 16u + 16u * nb) * 8u);
+            hmac_finish(h, 1u, fin, fin, opad);
+            const uint32_t diff = (r0.x ^ bswap(h[0])) | (r0.y ^ bswap(h[1])) | (r0.z ^ bswap(h[2])) |
+                                  (r0.w ^ bswap(h[3])) | (r1.x ^ bswap(h[4])) | (r1.y ^ bswap(h[5])) |
+                                  (r1.z ^ bswap(h[6])) | (r1.w ^ bswap(h[7]));
             const uint32_t padn = last.w >> 24;     // PKCS7.unpad: n = data[-1]
             st = diff ? 2 : (padn > 16u ? 4 : 0);
             if (st == 0) {
                 outlen = 16u * nb - padn;
             } else {
                 if (st == 4) outlen = padn;   // authenticated pad byte, for the error message
-
-                const u32x4 z = {0u, 0u, 0u, 0u};
                 for (uint32_t i = 0; i < nb; ++i) st16(O + 16 * i, z);
             }
         }

@@ -203,10 +203,16 @@ __global__ void k_deframe_counts(const uint64_t *nflags_p, const uint64_t *pos, 
                                  uint64_t *counts) {
     const uint64_t nf = *nflags_p;
     counts[0] = nf > 1 ? nf - 1 : 0;
-    // what the loop keeps: from the last flag on, unless it is more than 2*HW_MTU
-    // long (:406-407); with no flag at all the buffer is dropped (:408-410)
+    // What the loop keeps for the next read (TCPInterface.py:391-411): after a
+    // pair it has cut the buffer at the pair's closing flag, so it holds the
+    // buffer from the last flag on; with a single flag it never cut it and
+    // holds everything, junk before the flag included.  It drops what it
+    // holds once that is longer than 2*HW_MTU (:406-407), and all of it when
+    // there is no flag (:408-410).
     uint64_t consumed = len;
-    if (nf > 0) {
+    if (nf == 1) {
+        consumed = len > 2ull * hw_mtu ? len : 0;
+    } else if (nf > 1) {
         const uint64_t last = pos[nf - 1];
         consumed = (len - last > 2ull * hw_mtu) ? len : last;
     }

@@ -64,6 +64,17 @@ def test_oracle_deframe_matches_reference_read_loop(wv):
     assert [f.hex() for f in got] == c["frames"]
 
 
+def test_oracle_lone_flag_across_reads(wv):
+    """Junk then a lone flag: the read loop keeps the whole buffer, or drops
+    all of it past 2*HW_MTU (fixtures from the reference's read loop)."""
+    for r in wv["deframe_lone_flag"]:
+        buf, got = b"", []
+        for ch in r["chunks"]:
+            fr, _, buf = ow.deframe(buf + b(ch), r["hw_mtu"])
+            got += fr
+        assert [f.hex() for f in got] == r["frames"], r["name"]
+
+
 def test_oracle_ifac(wv):
     for r in wv["ifac"]:
         m = ow.ifac_mask(b(r["raw"]), b(r["ifac"]), b(r["ifac_key"]))
@@ -123,6 +134,17 @@ def test_gpu_deframe_matches_reference_read_loop(wv):
     for ch in c["chunks"]:
         got += d.feed(b(ch))
     assert [f.hex() for f in got] == c["frames"]
+
+
+@pytest.mark.gpu
+def test_gpu_lone_flag_across_reads(wv):
+    from reticulum_amd import wire
+    for r in wv["deframe_lone_flag"]:
+        d = wire.Deframer(hw_mtu=r["hw_mtu"])
+        got = []
+        for ch in r["chunks"]:
+            got += d.feed(b(ch))
+        assert [f.hex() for f in got] == r["frames"], r["name"]
 
 
 @pytest.mark.gpu

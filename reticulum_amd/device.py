@@ -147,3 +147,98 @@ def map_hashes(data, out, salts, part_off=None, part_len=None, part_res=None, sd
     _native.check(lib.rt_map_hashes(ctx, _p(data), _p(part_off), _p(part_len), data.numel(), sdu, _p(salts),
                                     salts.shape[1], _p(part_res), salts.shape[0], guard, _p(out),
                                     _p(first_collision), n_parts, _stream(stream)))
+
+
+# ---------------------------------------------------------------- wire side --
+# Device-resident forms of reticulum_amd.wire (wire_kernels.hip): flat uint8
+# buffers, int64 offsets, int32 lengths, enqueued on the stream, no sync.
+
+def _ctx_of(t):
+    return _native.context(t.device.index)
+
+
+def hdlc_frame(pkt, pkt_off, pkt_len, out, frame_off, workspace=None, stream=None):
+    """HDLC framing (TCPInterface.py:44-53, 323) of n packets into ``out`` in
+    order: frame i = 7E || escape(packet i) || 7E at out[frame_off[i]:
+    frame_off[i+1]]; frame_off (n+1,) int64, frame_off[n] = total bytes; out
+    needs sum(2*len+2) bytes at most."""
+    _check_u8(pkt, out)
+    n = pkt_off.numel()
+    if pkt_len.numel() != n or frame_off.numel() != n + 1:
+        raise ValueError("shape mismatch")
+    lib = _native.load()
+    ws = workspace if workspace is not None else torch.empty(
+        int(lib.rt_hdlc_frame_workspace_bytes(n)), dtype=torch.uint8, device=pkt.device)
+    _native.check(lib.rt_hdlc_frame(_ctx_of(pkt), _p(pkt), _p(pkt_off), _p(pkt_len), n, _p(out), _p(frame_off),
+                                    _p(ws), _stream(stream)))
+
+
+def hdlc_deframe(buf, out, frame_off, frame_len, status, counts, hw_mtu=262144, ifac_size=0, workspace=None,
+                 stream=None):
+    """One pass of the HDLC read loop (TCPInterface.py:387-410) over ``buf``:
+    for each consecutive flag pair k (at most frame_off.numel() pairs) the
+    unescaped frame at out[frame_off[k]: frame_off[k] + frame_len[k]] with its
+    RT_FRAME_* status; counts (2,) int64 = [pairs, bytes consumed]."""
+    _check_u8(buf, out)
+    max_pairs = frame_off.numel()
+    if frame_len.numel() != max_pairs or status.numel() != max_pairs or counts.numel() < 2 or \
+            out.numel() < buf.numel():
+        raise ValueError("shape mismatch")
+    lib = _native.load()
+    ws = workspace if workspace is not None else torch.empty(
+        int(lib.rt_hdlc_deframe_workspace_bytes(buf.numel())), dtype=torch.uint8, device=buf.device)
+    _native.check(lib.rt_hdlc_deframe(_ctx_of(buf), _p(buf), buf.numel(), hw_mtu, ifac_size, _p(out), _p(frame_off),
+                                      _p(frame_len), _p(status), _p(counts), max_pairs, _p(ws), _stream(stream)))
+
+
+def ifac_mask(pkt, pkt_off, pkt_len, ifac, ifac_key, out, out_off, stream=None):
+    """Transport.transmit's IFAC step (Transport.py:1069-1101): packet i plus
+    its access code ifac[i] (n, ifac_size) -> pkt_len[i] + ifac_size masked
+    bytes at out[out_off[i]:]; ifac_key (K,) uint8, K <= 64."""
+    _check_u8(pkt, ifac, ifac_key, out)
+    n = pkt_off.numel()
+    if pkt_len.numel() != n or ifac.shape[0] != n or out_off.numel() != n:
+        raise ValueError("shape mismatch")
+    lib = _native.load()
+    _native.check(lib.rt_ifac_mask(_ctx_of(pkt), _p(pkt), _p(pkt_off), _p(pkt_len), _p(ifac), ifac.shape[1],
+                                   _p(ifac_key), ifac_key.numel(), _p(out), _p(out_off), n, _stream(stream)))
+
+
+def ifac_unmask(pkt, pkt_off, pkt_len, ifac_key, ifac_out, out, out_off, status, stream=None):
+    """Transport.inbound's IFAC step up to the signature check
+    (Transport.py:1441-1475): status[i] = 0 with the IFAC in ifac_out[i] (n,
+    ifac_size) and the unmasked packet (pkt_len[i] - ifac_size bytes) at
+    out[out_off[i]:], or 1 where the reference drops the packet first."""
+    _check_u8(pkt, ifac_key, ifac_out, out)
+    n = pkt_off.numel()
+    if pkt_len.numel() != n or ifac_out.shape[0] != n or out_off.numel() != n or status.numel() != n:
+        raise ValueError("shape mismatch")
+    lib = _native.load()
+    _native.check(lib.rt_ifac_unmask(_ctx_of(pkt), _p(pkt), _p(pkt_off), _p(pkt_len), ifac_out.shape[1],
+                                     _p(ifac_key), ifac_key.numel(), _p(ifac_out), _p(out), _p(out_off), _p(status),
+                                     n, _stream(stream)))
+
+
+def packet_unpack(pkt, pkt_off, pkt_len, fields, stream=None):
+    """Packet.unpack + get_hash (Packet.py:242-275, 342-353): fields (n, 96)
+    uint8 receives one rt_packet_fields record per packet
+    (reticulum_amd.wire.FIELDS_DTYPE)."""
+    _check_u8(pkt, fields)
+    n = pkt_off.numel()
+    if pkt_len.numel() != n or fields.numel() != 96 * n:
+        raise ValueError("shape mismatch")
+    lib = _native.load()
+    _native.check(lib.rt_packet_unpack(_ctx_of(pkt), _p(pkt), _p(pkt_off), _p(pkt_len), _p(fields), n,
+                                       _stream(stream)))
+
+
+def pack_headers(flags, hops, destination_hash, context, out, out_off, transport_id=None, stream=None):
+    """Packet.pack's header (Packet.py:167-228) for n packets at
+    out[out_off[i]:]: flags, hops, [transport_id], destination hash, context
+    (19 or 35 bytes).  flags/hops/context (n,) uint8; hashes (n, 16) uint8."""
+    _check_u8(flags, hops, destination_hash, context, out, transport_id)
+    n = flags.numel()
+    lib = _native.load()
+    _native.check(lib.rt_packet_pack_headers(_ctx_of(out), _p(flags), _p(hops), _p(transport_id),
+                                             _p(destination_hash), _p(context), _p(out), _p(out_off), n,
+                                             _stream(stream)))

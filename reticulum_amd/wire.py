@@ -8,7 +8,8 @@
 * ``pack_headers_batch``                    Packet.pack's header, Packet.py:167-228
 
 Host-buffer conveniences over librnstok's device kernels (wire_kernels.hip);
-``reticulum_amd.device`` has the device-resident forms.  No CPU fallback.
+``reticulum_amd.device`` has the device-resident forms (hdlc_frame, hdlc_deframe,
+ifac_mask, ifac_unmask, packet_unpack, pack_headers).  No CPU fallback.
 """
 import ctypes
 

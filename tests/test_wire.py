@@ -208,3 +208,69 @@ def test_gpu_unpack_and_pack(wv):
         assert (g is None) == (o is None)
         if g:
             assert g == {k: o[k] for k in g}
+
+
+@pytest.mark.gpu
+def test_gpu_device_forms_match_host_forms():
+    """reticulum_amd.device's tensor entry points give what the host
+    conveniences (and so the oracle) give, on one random batch."""
+    import torch
+    from reticulum_amd import device, wire
+    rng = np.random.Generator(np.random.PCG64(228))
+    pk = [rng.integers(0, 128, 2, dtype=np.uint8).tobytes() + rng.integers(0, 256, int(n), dtype=np.uint8).tobytes()
+          for n in rng.integers(30, 600, 700)]
+    lens = np.array([len(p) for p in pk], np.int32)
+    off = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
+    dev = torch.device("cuda", 0)
+    flat = torch.from_numpy(np.frombuffer(b"".join(pk), np.uint8).copy()).to(dev)
+    t_off, t_len = torch.from_numpy(off).to(dev), torch.from_numpy(lens).to(dev)
+    n = len(pk)
+    # framing, then deframing the stream
+    framed = torch.empty(int(2 * lens.sum() + 2 * n), dtype=torch.uint8, device=dev)
+    foff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    device.hdlc_frame(flat, t_off, t_len, framed, foff)
+    total = int(foff[-1])
+    host_stream, _ = wire.hdlc_frame_batch(pk)
+    assert framed[:total].cpu().numpy().tobytes() == host_stream
+    buf = framed[:total].clone()
+    pairs = 2 * n
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    d_off = torch.empty(pairs, dtype=torch.int64, device=dev)
+    d_len = torch.empty(pairs, dtype=torch.int32, device=dev)
+    d_st = torch.empty(pairs, dtype=torch.int32, device=dev)
+    cnt = torch.empty(2, dtype=torch.int64, device=dev)
+    device.hdlc_deframe(buf, out, d_off, d_len, d_st, cnt)
+    o, dl, ds = out.cpu().numpy().tobytes(), d_len.cpu().numpy(), d_st.cpu().numpy()
+    do = d_off.cpu().numpy()
+    k = int(cnt[0])
+    frames = [o[int(do[i]):int(do[i]) + int(dl[i])] for i in range(k) if ds[i] == wire.FRAME_OK]
+    assert frames == [p for p in pk if len(p) > 19] and int(cnt[1]) == total - 1
+    # IFAC mask / unmask
+    key_h = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+    ifacs = rng.integers(0, 256, (n, 8), dtype=np.uint8)
+    key = torch.from_numpy(np.frombuffer(key_h, np.uint8).copy()).to(dev)
+    ti = torch.from_numpy(ifacs).to(dev)
+    m_len = lens + 8
+    m_off = np.concatenate([[0], np.cumsum(m_len[:-1])]).astype(np.int64)
+    masked = torch.empty(int(m_len.sum()), dtype=torch.uint8, device=dev)
+    tm_off, tm_len = torch.from_numpy(m_off).to(dev), torch.from_numpy(m_len).to(dev)
+    device.ifac_mask(flat, t_off, t_len, ti, key, masked, tm_off)
+    mh = masked.cpu().numpy().tobytes()
+    got = [mh[int(a):int(a) + int(b)] for a, b in zip(m_off, m_len)]
+    assert got == wire.ifac_mask_batch(pk, [r.tobytes() for r in ifacs], key_h)
+    un = torch.empty_like(masked)
+    i_out = torch.empty((n, 8), dtype=torch.uint8, device=dev)
+    ust = torch.empty(n, dtype=torch.int32, device=dev)
+    device.ifac_unmask(masked, tm_off, tm_len, key, i_out, un, tm_off, ust)
+    uh = un.cpu().numpy().tobytes()
+    assert (ust.cpu().numpy() == 0).all() and torch.equal(i_out, ti)
+    assert [uh[int(a):int(a) + int(b)] for a, b in zip(m_off, lens)] == [bytes([p[0] & 0x7F]) + p[1:] for p in pk]
+    # unpack
+    fields = torch.empty((n, 96), dtype=torch.uint8, device=dev)
+    device.packet_unpack(flat, t_off, t_len, fields)
+    f = fields.cpu().numpy().view(wire.FIELDS_DTYPE).reshape(-1)
+    ref = wire.unpack_batch(pk)
+    for i in range(n):
+        assert bool(f[i]["ok"]) == (ref[i] is not None)
+        if ref[i]:
+            assert bytes(f[i]["packet_hash"]) == ref[i]["packet_hash"]

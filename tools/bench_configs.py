@@ -9,6 +9,10 @@ ident: 2^20 x 500 B with a fresh HKDF-derived key per packet (Identity.encrypt
       keying, Identity.py:837-846): times rt_hkdf (32 B shared key, 16 B
       salt -> 64 B), the derived keyset (HKDF + key setup, incl. allocation)
       and encrypt / decrypt with key_idx = packet index
+wire: the interface path around the token, 2^20 raw
+      500-B packets on the device: HDLC framing into one stream, deframing
+      that stream (the read loop), IFAC mask and unmask (16-B IFACs, 64-B
+      key), Packet.unpack + packet hash; one line with every stage
 c5  : 2^20 packets (the per-GPU share of 8 M at 8 GPUs), lengths uniform in
       64..4096 B, 65 536 keys, 50/50 encrypt / decrypt (decrypt inputs are
       valid tokens produced by the encrypt kernel beforehand)
@@ -139,6 +143,9 @@ def main():
         bytes_pt = int(lens.sum())
         n_enc, n_dec = len(e_idx), len(d_idx)
         check = lambda: bool((st[: len(d_idx)] == 0).all())  # noqa: E731
+    elif cfg == "wire":
+        print(json.dumps(wire_config(dev, g, args.steps)))
+        return
     else:
         raise SystemExit("unknown config " + cfg)
 
@@ -165,6 +172,70 @@ def main():
                 "plaintext_gib_per_step": bytes_pt / 2**30,
                 "gib_s": (bytes_pt if cfg == "c5" else 2 * bytes_pt) / ((em + dm) * 1e-3) / 2**30})
     print(json.dumps(res))
+
+
+def wire_config(dev, g, steps):
+    import torch
+    from reticulum_amd import device
+    n, L, isz = 1 << 20, 500, 16
+    raw = torch.randint(0, 256, (n, L), dtype=torch.uint8, device=dev, generator=g)
+    raw[:, 1] &= 0x7F                                       # hops < PATHFINDER_M: every packet unpacks
+    flat = raw.reshape(-1)
+    off = torch.arange(n, dtype=torch.int64, device=dev) * L
+    ln = torch.full((n,), L, dtype=torch.int32, device=dev)
+    framed = torch.empty(n * (2 * L + 2), dtype=torch.uint8, device=dev)
+    foff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    device.hdlc_frame(flat, off, ln, framed, foff)
+    torch.cuda.synchronize()
+    total = int(foff[-1])
+    stream_buf = framed[:total].clone()
+    pairs = 2 * n                                            # frames and the empty gaps 7E|7E between them
+    dout = torch.empty(total, dtype=torch.uint8, device=dev)
+    d_off = torch.empty(pairs, dtype=torch.int64, device=dev)
+    d_len = torch.empty(pairs, dtype=torch.int32, device=dev)
+    d_st = torch.empty(pairs, dtype=torch.int32, device=dev)
+    cnt = torch.empty(2, dtype=torch.int64, device=dev)
+    ifac = torch.randint(0, 256, (n, isz), dtype=torch.uint8, device=dev, generator=g)
+    key = torch.randint(0, 256, (64,), dtype=torch.uint8, device=dev, generator=g)
+    ml = L + isz
+    masked = torch.empty(n * ml, dtype=torch.uint8, device=dev)
+    m_off = torch.arange(n, dtype=torch.int64, device=dev) * ml
+    m_len = torch.full((n,), ml, dtype=torch.int32, device=dev)
+    un = torch.empty(n * ml, dtype=torch.uint8, device=dev)
+    ifac_out = torch.empty((n, isz), dtype=torch.uint8, device=dev)
+    u_st = torch.empty(n, dtype=torch.int32, device=dev)
+    fields = torch.empty((n, 96), dtype=torch.uint8, device=dev)
+    stages = {
+        "hdlc_frame": (lambda: device.hdlc_frame(flat, off, ln, framed, foff), n * L),
+        "hdlc_deframe": (lambda: device.hdlc_deframe(stream_buf, dout, d_off, d_len, d_st, cnt), total),
+        "ifac_mask": (lambda: device.ifac_mask(flat, off, ln, ifac, key, masked, m_off), n * L),
+        "ifac_unmask": (lambda: device.ifac_unmask(masked, m_off, m_len, key, ifac_out, un, m_off, u_st), n * ml),
+        "packet_unpack": (lambda: device.packet_unpack(flat, off, ln, fields), n * L),
+    }
+    for f, _ in stages.values():
+        f()
+    torch.cuda.synchronize()
+    # size-independent checks: deframing returns every packet, unmasking inverts masking
+    rows = torch.randint(0, n, (4096,), device=dev, generator=g)
+    ok_frames = (int(cnt[0]) == pairs - 1 and int((d_st[0::2] == 0).sum()) == n and bool((d_len[0::2] == L).all()))
+    idx = d_off[0::2][rows].unsqueeze(1) + torch.arange(L, device=dev)
+    ok_frames = ok_frames and torch.equal(dout[idx], raw[rows])
+    back = un.view(n, ml)[:, :L]
+    ok_ifac = bool((u_st == 0).all()) and torch.equal(ifac_out, ifac) and torch.equal(back[:, 1:], raw[:, 1:]) and \
+        torch.equal(back[:, 0], raw[:, 0] & 0x7F)
+    ok_unpack = bool((fields[:, 0] == 1).all())
+    res = {"config": "wire", "packets": n, "packet_bytes": L, "ifac_size": isz,
+           "ok": bool(ok_frames and ok_ifac and ok_unpack), "stages": {}}
+    for name, (f, nbytes) in stages.items():
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for a, b in ev:
+            a.record()
+            f()
+            b.record()
+        torch.cuda.synchronize()
+        ms = sorted(a.elapsed_time(b) for a, b in ev)[steps // 2]
+        res["stages"][name] = {"ms": ms, "packets_s": n / (ms * 1e-3), "input_gb_s": nbytes / (ms * 1e-3) / 1e9}
+    return res
 
 
 if __name__ == "__main__":

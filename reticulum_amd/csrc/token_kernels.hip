@@ -382,6 +382,160 @@ __global__ __launch_bounds__(256) void k_encrypt_long(EncArgs a) {
     }
 }
 
+// ------------------------------------ encrypt, long tokens, 4 lanes/token --
+//
+// c4 sharded over 8 GPUs leaves 128 tokens of 16 KiB per CU, and a token's
+// CBC chain (1025 blocks x NR rounds, each round waiting on its table
+// lookups) is the critical path.  Here a quad of lanes carries one chain:
+// lane j owns column j of the state and looks up the four bytes of ITS column
+// word (T0[s_j.b0] feeds column j, T1[s_j.b1] column j-1, T2[s_j.b2] column
+// j-2, T3[s_j.b3] column j-3), then gathers the other three terms of its
+// column from the quad with DPP quad permutes: 3 addresses + 4 lookups + 4
+// XORs per lane and round instead of 16 + 16 + 8, so a round costs one LDS
+// round trip plus a few VALU cycles.  Waves 0-7 run the chains of 128 tokens
+// (16 per wave) and drop each quad of ciphertext into a two-slot LDS ring;
+// waves 8-9 hash the previous quad of the same tokens, one token per lane,
+// one barrier per quad step.  Single key, uniform lengths.
+constexpr uint32_t L4_TOK = 128, L4_AES_WAVES = 8, L4_THREADS = 64u * (L4_AES_WAVES + 2u);
+constexpr uint32_t L4_RING = LDS_ENC_BYTES;                              // after the table image
+constexpr uint32_t LDS_ENC_LONG4_BYTES = L4_RING + 2u * L4_TOK * 64u;     // + 2 slots x 128 tokens x 64 B
+
+// DPP quad_perm: lane j of each group of four reads lane (j + K) & 3.
+template <int K>
+__device__ __forceinline__ uint32_t quad_rot(uint32_t v) {
+    constexpr int ctrl = K == 1 ? 0x39 : (K == 2 ? 0x4E : 0x93);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t ld32u(const uint8_t *p) {
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+}
+__device__ __forceinline__ void st32u(uint8_t *p, uint32_t v) { __builtin_memcpy(p, &v, 4); }
+
+// Column `col` (bytes 4col..4col+3) of the PKCS7 pad block with r payload bytes at p.
+__device__ __forceinline__ uint32_t pad_col(const uint8_t *p, uint32_t r, uint32_t col) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t i = 4u * col + (uint32_t)k;
+        w |= (i < r ? (uint32_t)p[i] : 16u - r) << (8 * k);
+    }
+    return w;
+}
+
+// One block of the chain on a quad of lanes: s = this lane's column of
+// plaintext ^ previous ciphertext, rk = this lane's round-key column;
+// returns this lane's ciphertext column.
+template <int NR>
+__device__ __forceinline__ uint32_t enc_block4(uint32_t s, const uint32_t *rk, const Lanes &L) {
+    s ^= rk[0];
+#pragma unroll
+    for (int r = 1; r < NR; ++r) {
+        const uint32_t u0 = lds(taddr<0, 0>(s, L), 0), u1 = lds(taddr<1, 0>(s, L), 128);
+        const uint32_t u2 = lds(taddr<2, 1>(s, L), 0), u3 = lds(taddr<3, 1>(s, L), 128);
+        s = u0 ^ rk[r] ^ quad_rot<1>(u1) ^ quad_rot<2>(u2) ^ quad_rot<3>(u3);
+    }
+    // final round: byte k of column j is S[s_{j+k}.b_k] (tlast_enc, split the same way)
+    const uint32_t v0 = lds(taddr<0, 1>(s, L), 0) & 0x000000ffu, v1 = lds(taddr<1, 1>(s, L), 128) & 0x0000ff00u;
+    const uint32_t v2 = lds(taddr<2, 0>(s, L), 0) & 0x00ff0000u, v3 = lds(taddr<3, 0>(s, L), 128) & 0xff000000u;
+    return v0 ^ rk[NR] ^ quad_rot<1>(v1) ^ quad_rot<2>(v2) ^ quad_rot<3>(v3);
+}
+
+template <int NR>
+__global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
+    typedef __attribute__((address_space(3))) uint32_t lds_w;
+    typedef __attribute__((address_space(3))) const u32x4 lds_q;
+    fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);
+    const Lanes LN(threadIdx.x & 31u);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const bool aes = wave < L4_AES_WAVES;
+    const uint32_t col = threadIdx.x & 3u;
+    const uint32_t slot = aes ? threadIdx.x >> 2 : (wave - L4_AES_WAVES) * 64u + lane;   // token of the workgroup
+    const uint32_t L = a.uni_len, nfull = L >> 4, nq = nfull >> 2, tb = (nfull & 3u) + 1u, rem = L & 15u;
+    uint32_t rk[NR + 1];
+#pragma unroll
+    for (int r = 0; r <= NR; ++r) rk[r] = aes ? a.rec[REC_ENC + 4 * r + col] : 0u;
+
+    for (uint32_t base = blockIdx.x * L4_TOK; base < a.n; base += gridDim.x * L4_TOK) {
+        const uint32_t t = base + slot;
+        const bool valid = t < a.n;
+        const uint32_t p = valid ? (a.order ? a.order[t] : t) : 0u;
+        const uint8_t *P = a.pt + (valid ? in_off(a.pt_off, a.pt_stride, p) : 0);
+        uint8_t *O = a.tok + (valid ? in_off(a.tok_off, a.tok_stride, p) : 0);
+        if (aes) {
+            // this lane's column of the plaintext blocks of quad k (the tail quad: tb blocks, the last padded)
+            auto load_quad = [&](uint32_t k, uint32_t x[4]) {
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const uint8_t *B = P + 16ull * (4u * k + (uint32_t)b);
+                    x[b] = !valid ? 0u
+                                  : ((k < nq || (uint32_t)b + 1u < tb) ? ld32u(B + 4u * col)
+                                                                        : ((uint32_t)b + 1u == tb ? pad_col(B, rem, col) : 0u));
+                }
+            };
+            uint32_t prev = valid ? ld32u(a.iv + 16ull * p + 4u * col) : 0u, xn[4];
+            if (valid) st32u(O + 4u * col, prev);
+            load_quad(0u, xn);
+            for (uint32_t k = 0; k <= nq; ++k) {
+                const uint32_t x[4] = {xn[0], xn[1], xn[2], xn[3]};
+                if (k < nq) load_quad(k + 1u, xn);        // the next quad is requested before this quad's rounds
+                uint32_t cq[4];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    cq[b] = enc_block4<NR>(x[b] ^ prev, rk, LN);
+                    prev = cq[b];
+                }
+                const uint32_t nst = k < nq ? 4u : tb;
+                uint8_t *Ck = O + 16 + 64ull * k + 4u * col;
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (valid && (uint32_t)b < nst) st32u(Ck + 16 * b, cq[b]);
+                lds_w *ring = (lds_w *)(uintptr_t)(L4_RING + ((k & 1u) * L4_TOK + slot) * 64u + 4u * col);
+#pragma unroll
+                for (int b = 0; b < 4; ++b) ring[4 * b] = cq[b];
+                __syncthreads();     // quad k visible to the hashing waves; they are done with slot (k-1)&1
+            }
+            __syncthreads();         // matches the hashing waves' last step
+        } else {
+            uint32_t h[8], opad[8];
+            load_uniform8(h, a.rec + REC_IPAD);
+            load_uniform8(opad, a.rec + REC_OPAD);
+            u32x4 prev = valid ? ld16(a.iv + 16ull * p) : u32x4{0u, 0u, 0u, 0u};
+            const uint64_t bits = (uint64_t)(64u + 16u + 16u * (nfull + 1u)) * 8u;
+            __syncthreads();         // step 0: nothing to hash yet
+            for (uint32_t k = 1; k <= nq + 1u; ++k) {
+                lds_q *r = (lds_q *)(uintptr_t)(L4_RING + (((k - 1u) & 1u) * L4_TOK + slot) * 64u);
+                const u32x4 c0 = r[0], c1 = r[1], c2 = r[2], c3 = r[3];
+                if (k - 1u < nq) {
+                    uint32_t w[16];
+                    sha_units(w, prev, c0, c1, c2);
+                    sha256_compress(h, w);
+                    prev = c3;
+                } else if (valid) {
+                    // tail quad: units prev, c0..c_{tb-1} (+ final padding), then the outer hash
+                    const uint32_t tu = tb + 1u;
+                    if (tu >= 4u) {
+                        uint32_t w[16];
+                        sha_units(w, prev, c0, c1, c2);
+                        sha256_compress(h, w);
+                        sha_final_units(h, tu - 4u, c3, c3, c3, bits);
+                    } else {
+                        sha_final_units(h, tu, prev, c0, c1, bits);
+                    }
+                    uint32_t tag[8];
+                    hmac_outer(tag, h, opad);
+                    uint8_t *T = O + 16 + 16ull * (nfull + 1u);
+                    st16(T, u32x4{bswap(tag[0]), bswap(tag[1]), bswap(tag[2]), bswap(tag[3])});
+                    st16(T + 16, u32x4{bswap(tag[4]), bswap(tag[5]), bswap(tag[6]), bswap(tag[7])});
+                }
+                __syncthreads();
+            }
+        }
+    }
+}
+
 // --------------------------------------------------------------- decrypt --
 
 template <int NR, bool PERKEY>
@@ -828,7 +982,19 @@ static bool use_long(uint32_t n, const uint32_t *len, uint32_t uni, int n_cu) {
     return len == nullptr && uni >= 1024u && (uint64_t)n <= 128ull * (uint64_t)n_cu;
 }
 
+template <int NR>
+static hipError_t launch_enc_long4_nr(const EncArgs &a, int n_cu, hipStream_t s) {
+    uint64_t grid = (a.n + L4_TOK - 1ull) / L4_TOK;
+    if (grid > (uint64_t)n_cu) grid = n_cu;
+    hipLaunchKernelGGL((k_encrypt_long4<NR>), dim3((unsigned)grid), dim3(L4_THREADS), LDS_ENC_LONG4_BYTES, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_encrypt(const EncArgs &a, int nr, int n_cu, hipStream_t s) {
+#ifndef RNSTOK_NO_LONG4
+    if (!a.key_idx && use_long(a.n, a.pt_len, a.uni_len, n_cu))
+        return nr == 14 ? launch_enc_long4_nr<14>(a, n_cu, s) : launch_enc_long4_nr<10>(a, n_cu, s);
+#endif
     if (use_long(a.n, a.pt_len, a.uni_len, n_cu))
         return nr == 14 ? launch_enc_long_nr<14>(a, n_cu, s) : launch_enc_long_nr<10>(a, n_cu, s);
     const Shape sh = shape_for(a.n, a.key_idx ? WG_PERKEY_ENC : WG_ENC, n_cu);
@@ -874,6 +1040,8 @@ hipError_t configure_kernels() {
     RT_CFG((k_encrypt<10, true>), LDS_ENC_BYTES);
     RT_CFG((k_decrypt_long<14>), LDS_DEC_BYTES);
     RT_CFG((k_decrypt_long<10>), LDS_DEC_BYTES);
+    RT_CFG((k_encrypt_long4<14>), LDS_ENC_LONG4_BYTES);
+    RT_CFG((k_encrypt_long4<10>), LDS_ENC_LONG4_BYTES);
     RT_CFG((k_encrypt_long<14, false>), LDS_ENC_LONG_BYTES);
     RT_CFG((k_encrypt_long<14, true>), LDS_ENC_LONG_BYTES);
     RT_CFG((k_encrypt_long<10, false>), LDS_ENC_LONG_BYTES);

@@ -31,6 +31,7 @@ namespace {
 constexpr uint8_t FLAG = 0x7E, ESC = 0x7D, ESC_MASK = 0x20;
 constexpr uint32_t HEADER_MINSIZE = 19, DST_LEN = 16, PATHFINDER_M = 128;
 constexpr uint32_t SCAN_BLOCK = 1024;
+constexpr uint32_t WAVE_GRID = 16384;        // workgroups of the wave-per-frame kernels (grid-stride beyond)
 
 __device__ const uint32_t SHA_IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                                        0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
@@ -84,38 +85,100 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_add(uint64_t *out, const ui
     if (total_out && i == 0) *total_out = part[(n + SCAN_BLOCK - 1) / SCAN_BLOCK];
 }
 
+// ---------------------------------------------------- wave-level helpers --
+//
+// The framing kernels give each packet (frame) to one wave: its lanes cover
+// 4 consecutive bytes each of a 256-byte window, so loads and stores are
+// contiguous across the wave; escapes are found with byte-parallel compares
+// and output positions with a wave prefix sum.
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    const uint32_t l = threadIdx.x & 63u;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (l >= (uint32_t)d) x += y;
+    }
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
+    return x;
+}
+// little-endian word of p[i, i+4), bytes at or past `end` read as 0
+__device__ __forceinline__ uint32_t ld4_upto(const uint8_t *p, uint64_t i, uint64_t end) {
+    if (i + 4 <= end) {
+        uint32_t v;
+        __builtin_memcpy(&v, p + i, 4);
+        return v;
+    }
+    uint32_t v = 0;
+    for (uint32_t k = 0; k < 4; ++k)
+        if (i + k < end) v |= (uint32_t)p[i + k] << (8 * k);
+    return v;
+}
+__device__ __forceinline__ void st4u(uint8_t *p, uint32_t v) { __builtin_memcpy(p, &v, 4); }
+// 0x80 in every byte of x equal to the byte replicated in c4 (exact: no borrow crosses bytes)
+__device__ __forceinline__ uint32_t eqbytes(uint32_t x, uint32_t c4) {
+    const uint32_t t = x ^ c4;
+    return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
+}
+__device__ __forceinline__ uint32_t escbytes(uint32_t x) { return eqbytes(x, 0x7E7E7E7Eu) | eqbytes(x, 0x7D7D7D7Du); }
+
 // ------------------------------------------------------------- framing --
 
 __global__ __launch_bounds__(256) void k_hdlc_count(const uint8_t *pkt, const uint64_t *off, const uint32_t *len,
                                                     uint64_t *flen, uint32_t n) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint8_t *p = pkt + off[i];
-    const uint32_t L = len[i];
-    uint32_t extra = 0;
-    for (uint32_t k = 0; k < L; ++k) extra += (p[k] == FLAG || p[k] == ESC);
-    flen[i] = 2ull + L + extra;                      // 7E || escape(p) || 7E
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t i = w0; i < n; i += nw) {
+        const uint8_t *p = pkt + off[i];
+        const uint32_t L = len[i];
+        uint32_t extra = 0;
+        for (uint32_t b = 4u * lane; b < L; b += 256u) extra += __builtin_popcount(escbytes(ld4_upto(p, b, L)));
+        extra = wave_sum(extra);
+        if (lane == 0) flen[i] = 2ull + L + extra;     // 7E || escape(p) || 7E
+    }
 }
 
 __global__ __launch_bounds__(256) void k_hdlc_write(const uint8_t *pkt, const uint64_t *off, const uint32_t *len,
                                                     const uint64_t *foff, uint8_t *out, uint32_t n) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint8_t *p = pkt + off[i];
-    uint8_t *o = out + foff[i];
-    const uint32_t L = len[i];
-    uint64_t w = 0;
-    o[w++] = FLAG;
-    for (uint32_t k = 0; k < L; ++k) {       // HDLC.escape: ESC first, then FLAG (TCPInterface.py:50-52)
-        const uint8_t b = p[k];
-        if (b == ESC || b == FLAG) {
-            o[w++] = ESC;
-            o[w++] = b ^ ESC_MASK;
-        } else {
-            o[w++] = b;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t i = w0; i < n; i += nw) {
+        const uint8_t *p = pkt + off[i];
+        uint8_t *o = out + foff[i];
+        const uint32_t L = len[i];
+        if (lane == 0) o[0] = FLAG;
+        uint64_t base = 1;                       // output position of the window's first byte
+        for (uint32_t w = 0; w < L; w += 256u) {
+            const uint32_t b = w + 4u * lane;
+            const uint32_t nb = b < L ? min(4u, L - b) : 0u;
+            const uint32_t x = nb ? ld4_upto(p, b, L) : 0u;
+            const uint32_t esc = __builtin_popcount(escbytes(x));
+            const uint32_t sz = nb + esc;
+            const uint32_t incl = wave_incl_scan(sz);
+            uint8_t *q = o + base + (incl - sz);
+            if (esc == 0 && nb == 4) {
+                st4u(q, x);
+            } else {
+                // HDLC.escape: ESC first, then FLAG (TCPInterface.py:50-52); per byte the same
+                uint32_t wpos = 0;
+                for (uint32_t k = 0; k < nb; ++k) {
+                    const uint8_t c = (uint8_t)(x >> (8 * k));
+                    if (c == ESC || c == FLAG) {
+                        q[wpos++] = ESC;
+                        q[wpos++] = c ^ ESC_MASK;
+                    } else {
+                        q[wpos++] = c;
+                    }
+                }
+            }
+            base += __shfl(incl, 63, 64);
         }
+        if (lane == 0) o[base] = FLAG;
     }
-    o[w] = FLAG;
 }
 
 // ----------------------------------------------------------- deframing --
@@ -125,8 +188,9 @@ constexpr uint32_t FLAG_CHUNK = 4096;        // stream bytes per workgroup (256 
 __global__ __launch_bounds__(256) void k_flag_count(const uint8_t *buf, uint64_t len, uint64_t *cnt) {
     const uint64_t base = (uint64_t)blockIdx.x * FLAG_CHUNK + threadIdx.x * 16ull;
     uint32_t c = 0;
-    for (uint32_t k = 0; k < 16; ++k)
-        if (base + k < len) c += buf[base + k] == FLAG;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k += 4)
+        if (base + k < len) c += __builtin_popcount(eqbytes(ld4_upto(buf, base + k, len), 0x7E7E7E7Eu));
     __shared__ uint32_t s;
     if (threadIdx.x == 0) s = 0;
     __syncthreads();
@@ -138,9 +202,12 @@ __global__ __launch_bounds__(256) void k_flag_count(const uint8_t *buf, uint64_t
 __global__ __launch_bounds__(256) void k_flag_scatter(const uint8_t *buf, uint64_t len, const uint64_t *cnt_off,
                                                       uint64_t *pos) {
     const uint64_t base = (uint64_t)blockIdx.x * FLAG_CHUNK + threadIdx.x * 16ull;
-    uint32_t c = 0;
-    for (uint32_t k = 0; k < 16; ++k)
-        if (base + k < len) c += buf[base + k] == FLAG;
+    uint32_t m[4], c = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        m[k] = base + 4 * k < len ? eqbytes(ld4_upto(buf, base + 4 * k, len), 0x7E7E7E7Eu) : 0u;
+        c += __builtin_popcount(m[k]);
+    }
     // in-order rank of this thread's flags inside the chunk
     __shared__ uint32_t sh[256];
     sh[threadIdx.x] = c;
@@ -152,14 +219,19 @@ __global__ __launch_bounds__(256) void k_flag_scatter(const uint8_t *buf, uint64
         __syncthreads();
     }
     uint64_t w = cnt_off[blockIdx.x] + sh[threadIdx.x] - c;
-    for (uint32_t k = 0; k < 16; ++k)
-        if (base + k < len && buf[base + k] == FLAG) pos[w++] = base + k;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+        for (uint32_t f = m[k]; f; f &= f - 1) pos[w++] = base + 4 * k + (__builtin_ctz(f) >> 3);
 }
 
-// One lane per consecutive flag pair (k, k+1): the read loop's frame
+// One wave per consecutive flag pair (k, k+1): the read loop's frame
 // buf[pos_k+1 : pos_{k+1}) with its two bytes.replace passes (TCPInterface.py:
 // 397-398: ESC,5E -> 7E first, then ESC,5D -> 7D, each left to right and
-// non-overlapping), written at out + pos_k + 1.
+// non-overlapping), written at out + pos_k + 1.  Neither pattern can overlap
+// itself and a 7D is never the byte a replacement removes, so the two passes
+// are one local rule: byte i is dropped when byte i-1 is 7D and byte i is 5E
+// or 5D; a kept 7D followed by 5E becomes 7E.  Kept bytes are placed with a
+// wave prefix sum.
 __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, const uint64_t *pos, const uint64_t *nflags_p,
                                                        uint64_t max_pairs, uint32_t hw_mtu, uint32_t ifac_size,
                                                        uint8_t *out, uint64_t *frame_off, uint32_t *frame_len,
@@ -167,35 +239,53 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, const
     const uint64_t nf = *nflags_p;
     uint64_t npairs = nf > 1 ? nf - 1 : 0;
     if (npairs > max_pairs) npairs = max_pairs;
-    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < npairs;
-         k += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t k = w0; k < npairs; k += nw) {
         const uint64_t a = pos[k] + 1, e = pos[k + 1];
         uint8_t *o = out + a;
-        uint64_t w = 0;
-        for (uint64_t r = a; r < e;) {                     // pass 1
-            if (buf[r] == ESC && r + 1 < e && buf[r + 1] == (FLAG ^ ESC_MASK)) {
-                o[w++] = FLAG;
-                r += 2;
-            } else {
-                o[w++] = buf[r++];
+        uint64_t kept_total = 0;
+        uint32_t carry = 0;                       // last byte of the previous window
+        for (uint64_t w = a; w < e; w += 256u) {
+            const uint64_t b = w + 4u * lane;
+            const uint32_t nb = b < e ? (uint32_t)min((uint64_t)4, e - b) : 0u;
+            const uint32_t x = nb ? ld4_upto(buf, b, e) : 0u;
+            uint32_t prevb = __shfl_up(x, 1, 64) >> 24;
+            if (lane == 0) prevb = carry;
+            uint32_t nextb = __shfl_down(x, 1, 64) & 0xFFu;
+            if (lane == 63) nextb = b + 4 < e ? buf[b + 4] : 0u;
+            uint32_t outw = 0, kept = 0;
+            for (uint32_t j = 0; j < nb; ++j) {
+                const uint32_t c = (x >> (8 * j)) & 0xFFu;
+                const uint32_t pc = j ? (x >> (8 * (j - 1))) & 0xFFu : prevb;
+                const uint32_t nc = j < 3 ? (x >> (8 * (j + 1))) & 0xFFu : nextb;
+                const bool has_prev = b + j > a, has_next = b + j + 1 < e;
+                const bool drop = has_prev && pc == ESC && (c == (FLAG ^ ESC_MASK) || c == (ESC ^ ESC_MASK));
+                if (!drop) {
+                    const uint32_t v = (c == ESC && has_next && nc == (FLAG ^ ESC_MASK)) ? FLAG : c;
+                    outw |= v << (8 * kept);
+                    ++kept;
+                }
             }
-        }
-        const uint64_t n1 = w;
-        w = 0;
-        for (uint64_t r = 0; r < n1;) {                    // pass 2, in place (w <= r)
-            if (o[r] == ESC && r + 1 < n1 && o[r + 1] == (ESC ^ ESC_MASK)) {
-                o[w++] = ESC;
-                r += 2;
+            const uint32_t incl = wave_incl_scan(kept);
+            uint8_t *q = o + kept_total + (incl - kept);
+            if (kept == 4) {
+                st4u(q, outw);
             } else {
-                o[w++] = o[r++];
+                for (uint32_t t = 0; t < kept; ++t) q[t] = (uint8_t)(outw >> (8 * t));
             }
+            kept_total += __shfl(incl, 63, 64);
+            carry = __shfl(x, 63, 64) >> 24;
         }
-        frame_off[k] = a;
-        frame_len[k] = (uint32_t)w;
-        // check_frame_len (TCPInterface.py:336-339); empty frames are skipped (:400)
-        status[k] = w == 0 ? RT_FRAME_EMPTY
-                           : ((w <= HEADER_MINSIZE || w > (uint64_t)hw_mtu + ifac_size) ? RT_FRAME_BAD_LEN
-                                                                                        : RT_FRAME_OK);
+        if (lane == 0) {
+            frame_off[k] = a;
+            frame_len[k] = (uint32_t)kept_total;
+            // check_frame_len (TCPInterface.py:336-339); empty frames are skipped (:400)
+            status[k] = kept_total == 0 ? RT_FRAME_EMPTY
+                                        : ((kept_total <= HEADER_MINSIZE || kept_total > (uint64_t)hw_mtu + ifac_size)
+                                               ? RT_FRAME_BAD_LEN
+                                               : RT_FRAME_OK);
+        }
     }
 }
 
@@ -303,7 +393,6 @@ __global__ __launch_bounds__(256) void k_ifac(IfacArgs a) {
     uint32_t phi[8], pho[8];
     key_midstates(prkb, 32, phi, pho);
     uint32_t t[8];
-    uint64_t w_out = 0;                                   // inbound: write position in the reassembled packet
     for (uint32_t b = 0; 32u * b < total; ++b) {
         // message T_{b-1} (32 B, none for b = 0) || counter byte
         uint32_t w[16], h[8];
@@ -322,9 +411,21 @@ __global__ __launch_bounds__(256) void k_ifac(IfacArgs a) {
         for (int k = 0; k < 8; ++k) h[k] = phi[k];
         sha256_compress(h, w);
         hmac_outer(t, h, pho);
+        // mask bytes 32b .. 32b+31 of the (masked) packet
+        const uint32_t lo = 32u * b;
+        if (lo >= 2u + n && lo + 32u <= total) {
+            // inside the payload: 2 x 16 B, masked in place of the byte loop below
+            const u32x4 m0 = {bswap(t[0]), bswap(t[1]), bswap(t[2]), bswap(t[3])};
+            const u32x4 m1 = {bswap(t[4]), bswap(t[5]), bswap(t[6]), bswap(t[7])};
+            const uint8_t *src = MASK ? raw + (lo - n) : raw + lo;
+            uint8_t *dst = MASK ? o + lo : o + (lo - n);
+            st16(dst, ld16(src) ^ m0);
+            st16(dst + 16, ld16(src + 16) ^ m1);
+            continue;
+        }
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
-            const uint32_t pos = 32u * b + j;
+            const uint32_t pos = lo + j;
             if (pos >= total) continue;
             const uint8_t m = (uint8_t)(t[j >> 2] >> (24 - 8 * (j & 3)));
             if (MASK) {
@@ -335,9 +436,10 @@ __global__ __launch_bounds__(256) void k_ifac(IfacArgs a) {
                 else v = raw[pos - n] ^ m;
                 o[pos] = v;
             } else {
-                if (pos == 0) o[w_out++] = (uint8_t)((raw[0] ^ m) & 0x7Fu);
-                else if (pos == 1) o[w_out++] = raw[1] ^ m;
-                else if (pos >= 2u + n) o[w_out++] = raw[pos] ^ m;
+                // reassembled: [un0 & 0x7f, un1] || un[2+n:]
+                if (pos == 0) o[0] = (uint8_t)((raw[0] ^ m) & 0x7Fu);
+                else if (pos == 1) o[1] = raw[1] ^ m;
+                else if (pos >= 2u + n) o[pos - n] = raw[pos] ^ m;
             }
         }
     }
@@ -345,28 +447,39 @@ __global__ __launch_bounds__(256) void k_ifac(IfacArgs a) {
 
 // --------------------------------------------------------- packet header --
 
-// SHA-256 over  first || src[0..len)  (one modified leading byte, then bytes)
+// SHA-256 over  first || src[0..len): the full 64-B blocks from 16-B loads
+// at src - 1 (that byte is readable: the packet's hop count or the transport
+// id's last byte) with `first` put in front, the last block(s) byte by byte.
 __device__ void sha_prefixed(uint8_t first, const uint8_t *src, uint32_t len, uint32_t out[8]) {
     uint32_t h[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) h[k] = SHA_IV[k];
     const uint32_t m = len + 1u;
     const uint64_t bits = (uint64_t)m * 8u;
-    const uint32_t nblk = (m + 8u) / 64u + 1u;
-    for (uint32_t b = 0; b < nblk; ++b) {
+    const uint32_t nfull = m / 64u;
+    for (uint32_t b = 0; b < nfull; ++b) {
+        const uint8_t *B = src - 1 + 64ull * b;
+        uint32_t w[16];
+        sha_units(w, ld16(B), ld16(B + 16), ld16(B + 32), ld16(B + 48));
+        if (b == 0) w[0] = (w[0] & 0x00FFFFFFu) | ((uint32_t)first << 24);
+        sha256_compress(h, w);
+    }
+    const uint32_t r = m - 64u * nfull;                 // 0..63 message bytes left
+    const uint32_t nblk = (r + 8u) / 64u + 1u;
+    for (uint32_t bb = 0; bb < nblk; ++bb) {
         uint32_t w[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             uint32_t v = 0;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const uint32_t q = 64u * b + 4u * k + j;
+                const uint32_t q = 64u * (nfull + bb) + 4u * k + j;
                 const uint32_t byte = q == 0 ? first : (q < m ? src[q - 1] : (q == m ? 0x80u : 0u));
                 v = (v << 8) | byte;
             }
             w[k] = v;
         }
-        if (b + 1 == nblk) {
+        if (bb + 1 == nblk) {
             w[14] = (uint32_t)(bits >> 32);
             w[15] = (uint32_t)bits;
         }
@@ -456,7 +569,8 @@ hipError_t launch_hdlc_frame(const uint8_t *pkt, const uint64_t *off, const uint
     if (n == 0) return hipSuccess;
     uint64_t *flen = (uint64_t *)ws;
     uint64_t *part = flen + n;
-    const unsigned g = (n + 255) / 256;
+    // one wave per packet, grid-stride: 4 packets per 256-thread workgroup
+    const unsigned g = (unsigned)min((uint64_t)(n + 3) / 4, (uint64_t)WAVE_GRID);
     hipLaunchKernelGGL(k_hdlc_count, dim3(g), dim3(256), 0, s, pkt, off, len, flen, n);
     hipError_t e = launch_scan(flen, frame_off, n, part, frame_off + n, s);
     if (e != hipSuccess) return e;
@@ -488,8 +602,7 @@ hipError_t launch_hdlc_deframe(const uint8_t *buf, uint64_t len, uint32_t hw_mtu
     hipLaunchKernelGGL(k_deframe_counts, dim3(1), dim3(1), 0, s, nflags, pos, len, hw_mtu, counts);
     // the pair count lives on the device: a grid-stride kernel sized by the caller's capacity
     if (max_pairs) {
-        uint64_t g = (max_pairs + 255) / 256;
-        if (g > 4096) g = 4096;
+        const uint64_t g = min((max_pairs + 3) / 4, (uint64_t)WAVE_GRID);     // one wave per frame
         hipLaunchKernelGGL(k_hdlc_unescape, dim3((unsigned)g), dim3(256), 0, s, buf, pos, nflags, max_pairs, hw_mtu,
                            ifac_size, out, frame_off, frame_len, status);
     }

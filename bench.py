@@ -260,7 +260,9 @@ def main():
                              "1464/SHA-256 compression, +8 tag compare) / HIP-event kernel time; peak = CUs x 128 "
                              "lanes x 2.4 GHz (full-rate VALU); frac_of_survey_P uses BASELINE.md §5's P = CUs x 64 "
                              "x 2.4 GHz; traffic = HBM bytes per launch from the committed rocprofv3 PMC summary "
-                             "(profiles/*_pmc.json, FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM)"},
+                             "(profiles/*_pmc.json; see traffic.calibration). On gfx950 LDS lookups and VALU issue do not "
+                             "overlap (tools/overlap_probe.hip: their times add), so the kernel's floor is the LDS time "
+                             "plus the VALU time of its instruction mix (DESIGN.md §4.5)"},
         "cpu_baseline": cpu,
         "e2e_pcie": e2e,
     }
@@ -282,9 +284,15 @@ def traffic_from_profiles(kernel, n, L, keys):
             continue
         meta = d.get("_workload", {})
         if meta.get("packets") == n and meta.get("length") == L and meta.get("keys") == keys and kernel in d:
-            v = d[kernel].get("hbm_bytes_per_launch")
-            if v:
-                return {"bytes": v, "source": os.path.relpath(path, ROOT)}
+            raw = d[kernel].get("hbm_bytes_per_launch_uncorrected")
+            if raw:
+                return {"bytes": raw, "bytes_with_x2_fetch_correction": d[kernel].get("hbm_bytes_per_launch"),
+                        "source": os.path.relpath(path, ROOT),
+                        "calibration": "FETCH_SIZE + WRITE_SIZE as counted. The guide's x2 FETCH correction is for "
+                                       "coalesced 16-B streams (our control reads 0.50x its known bytes); on this "
+                                       "kernel's 500-B-stride lane pattern a pure read of a known 524 MB reports 1.40x "
+                                       "(tools/fetch_calib.hip, profiles/r01c_fetch_calib.txt), the encrypt kernel "
+                                       "1.32x of its algorithmic reads: no over-fetch beyond the access pattern's own"}
     return None
 
 

@@ -279,24 +279,28 @@ def test_sorted_variable_batch_matches_unsorted_and_oracle(rt):
         assert bh[coff[i]:coff[i] + lens[i]].tobytes() == buf[off[i]:off[i] + lens[i]].tobytes()
 
 
-@pytest.mark.parametrize("n,L", [(300, 1024), (300, 1500), (20000, 4095), (2048, 16391)])
-def test_long_token_mode_vs_oracle(rt, n, L):
+@pytest.mark.parametrize("n,L,klen", [(300, 1024, 64), (300, 1500, 64), (20000, 4095, 64), (2048, 16391, 64),
+                                       (1, 1024, 64), (129, 1039, 64), (257, 1036, 64), (300, 2047, 32),
+                                       (5000, 1055, 32), (64, 1064, 64)])
+def test_long_token_mode_vs_oracle(rt, n, L, klen):
     """Uniform batches of long tokens with few packets per CU take the
-    producer/consumer kernel (AES wave -> LDS ring -> SHA wave); bit-exact vs
-    the oracle for every tail shape, and decrypt round-trips."""
+    long-token kernels (single key: a quad of lanes per CBC chain, AES waves
+    -> LDS ring -> SHA waves); bit-exact vs the oracle for every tail shape
+    (tail quads of 1-4 blocks, pad of 1-16 bytes), ragged last workgroups,
+    AES-256 and AES-128, and decrypt round-trips."""
     import torch
     from reticulum_amd import device
-    rng = np.random.Generator(np.random.PCG64(L))
+    rng = np.random.Generator(np.random.PCG64(L + n))
     tl = rt.token_len(L)
     pt_h = rng.integers(0, 256, (n, L), dtype=np.uint8)
     iv_h = rng.integers(0, 256, (n, 16), dtype=np.uint8)
-    key = rng.integers(0, 256, 64, dtype=np.uint8)
+    key = rng.integers(0, 256, klen, dtype=np.uint8)
     ks = rt.KeySet(key.tobytes())
     pt = torch.from_numpy(pt_h).cuda()
     tok = torch.empty((n, tl), dtype=torch.uint8, device="cuda")
     device.encrypt_uniform(ks, pt, L, torch.from_numpy(iv_h).cuda(), tok)
     sel = np.unique(np.concatenate([np.arange(0, n, max(1, n // 40)), [n - 1]]))
-    ref, _, _ = _oracle_tokens(key.reshape(1, 64), pt_h[sel].reshape(-1), np.arange(len(sel), dtype=np.uint64) * L,
+    ref, _, _ = _oracle_tokens(key.reshape(1, klen), pt_h[sel].reshape(-1), np.arange(len(sel), dtype=np.uint64) * L,
                                np.full(len(sel), L, np.uint32), iv_h[sel], None)
     assert np.array_equal(ref.reshape(len(sel), tl), tok.cpu().numpy()[sel])
     back = torch.empty((n, tl - 48), dtype=torch.uint8, device="cuda")

@@ -181,14 +181,14 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
         uint32_t h[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) h[i] = ipad[i];
-        // One enc_quad instance serves every quad, the tail quad (tb blocks,
-        // the last one carrying the PKCS7 pad; unused slots run on zeros and
-        // are not stored) included; the SHA-256 compression of quad q-1's
-        // units rides on quad q's AES chain (quad 0's SHA slot hashes zeros
-        // and is dropped).  hmac_finish runs the last 2-3 compressions through
-        // one sha256_compress: one copy of each, 49 KB of code where a
-        // head/body/tail-specialised loop took 150 KB (same speed on c2,
-        // measured; 2-7 % faster with per-packet keys).
+        // One loop body serves every quad, the tail quad (tb blocks, the last
+        // one carrying the PKCS7 pad; unused slots run on zeros and are not
+        // stored) included; the SHA-256 compression of quad q-1's units rides
+        // on quad q's AES chain (quad 0 has none and runs the chain alone).
+        // hmac_finish runs the last 2-3 compressions through one
+        // sha256_compress: ≈75 KB of code where a head/body/tail-specialised
+        // loop took 150 KB (same speed on c2, measured; 2-7 % faster with
+        // per-packet keys).
         {
             const u32x4 z = {0u, 0u, 0u, 0u};
             const uint32_t rem = L & 15u;
@@ -207,7 +207,10 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
                                                      : ((uint32_t)j + 1u == tb ? pad_block(P + 16 * j, rem) : z);
                 }
                 S.start(h);
-                enc_quad<NR, true>(c, x, prev, K.rk, LN, S);
+                if (q == 0u)        // no SHA block yet: the AES chain alone (a second, SHA-free copy of the
+                    enc_quad<NR, false>(c, x, prev, K.rk, LN, S);     // quad; 4 % faster than hashing zeros)
+                else
+                    enc_quad<NR, true>(c, x, prev, K.rk, LN, S);
                 // The SHA rounds' results are consumed here, in the AES
                 // chain's block: otherwise the compiler sinks the rounds
                 // past the stores below and the two chains run back to back.

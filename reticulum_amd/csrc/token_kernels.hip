@@ -161,14 +161,14 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
 
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += nthreads) {
         const uint32_t p = a.order ? a.order[i] : i;
+        // the opad midstate is loaded after the quad loop, so it does not
+        // hold registers through it
+        const uint32_t *r = PERKEY ? a.rec + (uint64_t)a.key_idx[p] * REC_WORDS : a.rec;
         if (PERKEY) {
-            const uint32_t *r = a.rec + (uint64_t)a.key_idx[p] * REC_WORDS;
             K.load(r, REC_ENC);
             load8(ipad, r + REC_IPAD);
-            load8(opad, r + REC_OPAD);
         } else {
             load_uniform8(ipad, a.rec + REC_IPAD);
-            load_uniform8(opad, a.rec + REC_OPAD);
         }
         const uint32_t L = in.l(p);
         const uint8_t *P = a.pt + in.o(p);
@@ -238,6 +238,10 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
 #pragma unroll
             for (int k = 0; k < 16; ++k) u4[k] = tu >= 4u ? u4[k] : S.w[k];
             sha_final_block(fin, u4, tu >= 4u ? tu - 4u : tu, (uint64_t)(64u + 16u + 16u * (nfull + 1u)) * 8u);
+            if (PERKEY)
+                load8(opad, r + REC_OPAD);
+            else
+                load_uniform8(opad, a.rec + REC_OPAD);
             hmac_finish(h, tu >= 4u ? 0u : 1u, S.w, fin, opad);
             uint8_t *T = O + 16 + 16ull * (nfull + 1u);
             st16(T, u32x4{bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3])});
@@ -558,16 +562,14 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_DEC : WG_DEC) void k_decr
 
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += nthreads) {
         const uint32_t p = a.order ? a.order[i] : i;
-        const uint32_t *r = a.rec;
+        const uint32_t *r = PERKEY ? a.rec + (uint64_t)a.key_idx[p] * REC_WORDS : a.rec;
         if (PERKEY) {
-            r = a.rec + (uint64_t)a.key_idx[p] * REC_WORDS;
             K.load(r, REC_DEC);
             load8(ipad, r + REC_IPAD);
-            load8(opad, r + REC_OPAD);
         } else {
             load_uniform8(ipad, a.rec + REC_IPAD);
-            load_uniform8(opad, a.rec + REC_OPAD);
         }
+        // opad: loaded where it is used, after the quad loop
         const uint32_t T = in.l(p);
         const uint8_t *Kt = a.tok + in.o(p);
         uint8_t *O = a.pt + (a.pt_off ? a.pt_off[p] : (uint64_t)p * a.pt_stride);
@@ -582,6 +584,10 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_DEC : WG_DEC) void k_decr
             } else {
                 uint32_t h[8], tag[8];
                 for (int i = 0; i < 8; ++i) h[i] = ipad[i];
+                if (PERKEY)
+                    load8(opad, r + REC_OPAD);
+                else
+                    load_uniform8(opad, a.rec + REC_OPAD);
                 sha_bytes_after_ipad(h, Kt, T - 32u);
                 hmac_outer(tag, h, opad);
                 uint32_t diff = 0;
@@ -639,6 +645,10 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_DEC : WG_DEC) void k_decr
             uint32_t u[16], fin[16];
             sha_units(u, full ? c[3] : pb, c[0], c[1], z);
             sha_final_block(fin, u, full ? tu - 4u : tu, (uint64_t)(64u + 16u + 16u * nb) * 8u);
+            if (PERKEY)
+                load8(opad, r + REC_OPAD);
+            else
+                load_uniform8(opad, a.rec + REC_OPAD);
             hmac_finish(h, 1u, fin, fin, opad);
             const uint32_t diff = (r0.x ^ bswap(h[0])) | (r0.y ^ bswap(h[1])) | (r0.z ^ bswap(h[2])) |
                                   (r0.w ^ bswap(h[3])) | (r1.x ^ bswap(h[4])) | (r1.y ^ bswap(h[5])) |

@@ -286,7 +286,7 @@ int rt_encrypt_ex(const rt_keyset *k, const uint8_t *pt, const uint64_t *pt_off,
     if ((flags & RT_F_SORT_BY_LENGTH) && n > 1) {
         if (!workspace) return fail(RT_E_INVAL, "rt_encrypt_ex: RT_F_SORT_BY_LENGTH needs a workspace");
         RT_HIP(hipSetDevice(k->ctx->device), "hipSetDevice");
-        RT_HIP(launch_length_order(pt_len, n, 0, workspace, &a.order, k->ctx->n_cu, pick(k->ctx, stream)),
+        RT_HIP(launch_length_order(pt_len, n, 0, workspace, &a.order, &a.queue, k->ctx->n_cu, pick(k->ctx, stream)),
                "length order");
     }
     return enc_common(k, a, stream);
@@ -305,7 +305,7 @@ int rt_decrypt_ex(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_of
     if ((flags & RT_F_SORT_BY_LENGTH) && n > 1) {
         if (!workspace) return fail(RT_E_INVAL, "rt_decrypt_ex: RT_F_SORT_BY_LENGTH needs a workspace");
         RT_HIP(hipSetDevice(k->ctx->device), "hipSetDevice");
-        RT_HIP(launch_length_order(tok_len, n, 1, workspace, &a.order, k->ctx->n_cu, pick(k->ctx, stream)),
+        RT_HIP(launch_length_order(tok_len, n, 1, workspace, &a.order, &a.queue, k->ctx->n_cu, pick(k->ctx, stream)),
                "length order");
     }
     return dec_common(k, a, stream);

@@ -130,6 +130,29 @@ __device__ __forceinline__ void load8(uint32_t d[8], const uint32_t *p) {
     d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
 }
 
+// ---------------------------------------------------------- packet loop --
+//
+// One packet per lane.  Uniform batches use a static grid stride (every lane
+// gets the same work).  Length-ordered batches (a.queue set, packets sorted
+// by descending length) hand out 64-packet chunks from a global counter, one
+// atomic per wave and chunk: the longest packets start first and the chunks
+// that finish last are the shortest, so the CUs end together.  A static
+// stride over the sorted order gave the first workgroup the longest packet of
+// every pass (c5: 40 % more work than the average CU).
+__device__ __forceinline__ uint32_t take_chunk(uint32_t *q) {
+    uint32_t v = 0u;
+    if ((threadIdx.x & 63u) == 0u) v = __hip_atomic_fetch_add(q, 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readlane(v, 0);
+}
+// Lane 0 carries the wave's smallest index, so it stays active until the
+// whole wave leaves (lanes past n break out of the last chunk only).
+#define RT_PACKET_LOOP(A, I)                                                                              \
+    for (uint32_t rt_base_ = (A).queue ? take_chunk((A).queue) : blockIdx.x * blockDim.x + (threadIdx.x & ~63u), \
+                  I = rt_base_ + (threadIdx.x & 63u);                                                      \
+         rt_base_ < (A).n && I < (A).n;                                                                    \
+         rt_base_ = (A).queue ? take_chunk((A).queue) : rt_base_ + gridDim.x * blockDim.x,               \
+                  I = rt_base_ + (threadIdx.x & 63u))
+
 // PKCS7 pad block (PKCS7.py:35-39): r (< 16) payload bytes at p, then 16-r copies of 16-r.
 __device__ __forceinline__ u32x4 pad_block(const uint8_t *p, uint32_t r) {
     uint32_t n = 16u - r, w[4] = {0, 0, 0, 0};
@@ -157,9 +180,8 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
     uint32_t ipad[8], opad[8];
     if (!PERKEY) K.load(a.rec, REC_ENC);
     const Layout in{a.pt_off, a.pt_stride, a.pt_len, a.uni_len};
-    const uint32_t nthreads = gridDim.x * blockDim.x;
 
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += nthreads) {
+    RT_PACKET_LOOP(a, i) {
         const uint32_t p = a.order ? a.order[i] : i;
         // the opad midstate is loaded after the quad loop, so it does not
         // hold registers through it
@@ -558,9 +580,8 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_DEC : WG_DEC) void k_decr
     uint32_t ipad[8], opad[8];
     if (!PERKEY) K.load(a.rec, REC_DEC);
     const Layout in{a.tok_off, a.tok_stride, a.tok_len, a.uni_len};
-    const uint32_t nthreads = gridDim.x * blockDim.x;
 
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += nthreads) {
+    RT_PACKET_LOOP(a, i) {
         const uint32_t p = a.order ? a.order[i] : i;
         const uint32_t *r = PERKEY ? a.rec + (uint64_t)a.key_idx[p] * REC_WORDS : a.rec;
         if (PERKEY) {
@@ -840,10 +861,12 @@ __global__ __launch_bounds__(1024) void k_sort_scatter(const uint32_t *len, uint
 uint64_t sort_workspace_bytes(uint32_t n) { return ((uint64_t)n * 4 + 255) / 256 * 256 + 2ull * SORT_BUCKETS * 4; }
 
 hipError_t launch_length_order(const uint32_t *len, uint32_t n, int dec, void *workspace, const uint32_t **order,
-                               int n_cu, hipStream_t s) {
+                               uint32_t **queue, int n_cu, hipStream_t s) {
     uint32_t *ord = (uint32_t *)workspace;
     uint32_t *hist = (uint32_t *)((uint8_t *)workspace + ((uint64_t)n * 4 + 255) / 256 * 256);
-    hipError_t e = hipMemsetAsync(hist, 0, SORT_BUCKETS * 4, s);
+    // hist[0..SORT_BUCKETS) and the chunk counter right after it, zeroed together
+    hipError_t e = hipMemsetAsync(hist, 0, SORT_BUCKETS * 4 + 4, s);
+    *queue = hist + SORT_BUCKETS;
     if (e != hipSuccess) return e;
     const int gh = n_cu < (int)((n + 1023) / 1024) ? n_cu : (int)((n + 1023) / 1024);
     hipLaunchKernelGGL(k_sort_hist, dim3(gh > 0 ? gh : 1), dim3(1024), 0, s, len, n, dec, hist);

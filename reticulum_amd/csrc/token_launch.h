@@ -19,6 +19,7 @@ struct EncArgs {
     const uint64_t *tok_off;    // null -> i * tok_stride
     uint64_t tok_stride;
     const uint32_t *order;      // null -> lane i handles packet i; else packet order[i]
+    uint32_t *queue;            // null -> static grid stride; else a zeroed chunk counter (sorted batches)
     uint32_t n;
 };
 
@@ -37,6 +38,7 @@ struct DecArgs {
     uint32_t *out_len;
     int32_t *status;
     const uint32_t *order;      // null -> lane i handles token i; else token order[i]
+    uint32_t *queue;            // as EncArgs::queue
     uint32_t n;
 };
 
@@ -116,10 +118,12 @@ hipError_t configure_kernels();
 // Length bucketing: order[] = packet indices grouped by descending AES quad
 // count, so that the lanes of a wave carry similar lengths.  `dec` selects
 // token lengths (quads of the ciphertext body) instead of plaintext lengths.
+// *queue receives a zeroed chunk counter: the token kernels' waves then take
+// the ordered packets 64 at a time, longest first (dynamic balance).
 constexpr uint32_t SORT_BUCKETS = 4096;
 uint64_t sort_workspace_bytes(uint32_t n);    // order[n] + 2 x SORT_BUCKETS counters
 hipError_t launch_length_order(const uint32_t *len, uint32_t n, int dec, void *workspace, const uint32_t **order,
-                               int n_cu, hipStream_t s);
+                               uint32_t **queue, int n_cu, hipStream_t s);
 hipError_t launch_encrypt(const EncArgs &a, int nr, int n_cu, hipStream_t s);
 hipError_t launch_decrypt(const DecArgs &a, int nr, int n_cu, hipStream_t s);
 hipError_t launch_map_hashes(const MapArgs &m, hipStream_t s);

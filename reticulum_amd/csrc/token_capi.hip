@@ -8,6 +8,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <string>
 
@@ -25,7 +26,17 @@ struct rt_ctx {
     std::mutex mu;                 // serialises host-staging calls
     uint8_t *d_work = nullptr;     // host-path workspace
     uint64_t work_cap = 0;
+    // Chunk counters for the token kernels' dynamic packet loop (ragged
+    // uniform batches): one 64-B slot per launch, round-robin, zeroed on the
+    // launch's stream.  A slot is reused after QUEUE_SLOTS launches.
+    static constexpr uint32_t QUEUE_SLOTS = 1024;
+    uint32_t *d_queues = nullptr;
+    std::atomic<uint32_t> q_next{0};
 };
+
+static uint32_t *next_queue(rt_ctx *c) {
+    return c->d_queues ? c->d_queues + 16u * (c->q_next.fetch_add(1) % rt_ctx::QUEUE_SLOTS) : nullptr;
+}
 
 struct rt_keyset {
     rt_ctx *ctx = nullptr;
@@ -115,6 +126,7 @@ rt_ctx *rt_create(int device) {
     make_sbox(tables, tables + 256);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_sbox, 512) != hipSuccess ||
+        hipMalloc(&c->d_queues, 64ull * rt_ctx::QUEUE_SLOTS) != hipSuccess ||
         hipMemcpy(c->d_sbox, tables, 512, hipMemcpyHostToDevice) != hipSuccess) {
         fail(RT_E_HIP, "context setup failed");
         rt_destroy(c);
@@ -128,6 +140,7 @@ void rt_destroy(rt_ctx *c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     hipFree(c->d_sbox);
+    hipFree(c->d_queues);
     hipFree(c->d_work);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -213,7 +226,7 @@ static int enc_common(const rt_keyset *k, EncArgs &a, void *stream) {
     a.rec = k->d_rec;
     a.sbox = k->ctx->d_sbox;
     RT_HIP(hipSetDevice(k->ctx->device), "hipSetDevice");
-    RT_HIP(launch_encrypt(a, k->nr, k->ctx->n_cu, pick(k->ctx, stream)), "encrypt launch");
+    RT_HIP(launch_encrypt(a, k->nr, k->ctx->n_cu, next_queue(k->ctx), pick(k->ctx, stream)), "encrypt launch");
     return RT_OK;
 }
 
@@ -225,7 +238,7 @@ static int dec_common(const rt_keyset *k, DecArgs &a, void *stream) {
     a.rec = k->d_rec;
     a.sbox = k->ctx->d_sbox;
     RT_HIP(hipSetDevice(k->ctx->device), "hipSetDevice");
-    RT_HIP(launch_decrypt(a, k->nr, k->ctx->n_cu, pick(k->ctx, stream)), "decrypt launch");
+    RT_HIP(launch_decrypt(a, k->nr, k->ctx->n_cu, next_queue(k->ctx), pick(k->ctx, stream)), "decrypt launch");
     return RT_OK;
 }
 

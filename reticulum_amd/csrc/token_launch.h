@@ -124,8 +124,10 @@ constexpr uint32_t SORT_BUCKETS = 4096;
 uint64_t sort_workspace_bytes(uint32_t n);    // order[n] + 2 x SORT_BUCKETS counters
 hipError_t launch_length_order(const uint32_t *len, uint32_t n, int dec, void *workspace, const uint32_t **order,
                                uint32_t **queue, int n_cu, hipStream_t s);
-hipError_t launch_encrypt(const EncArgs &a, int nr, int n_cu, hipStream_t s);
-hipError_t launch_decrypt(const DecArgs &a, int nr, int n_cu, hipStream_t s);
+// spare_queue: a counter slot the launch may zero and use as a.queue when the
+// static stride would leave a ragged last pass (null: never).
+hipError_t launch_encrypt(const EncArgs &a, int nr, int n_cu, uint32_t *spare_queue, hipStream_t s);
+hipError_t launch_decrypt(const DecArgs &a, int nr, int n_cu, uint32_t *spare_queue, hipStream_t s);
 hipError_t launch_map_hashes(const MapArgs &m, hipStream_t s);
 hipError_t launch_hkdf(const HkdfArgs &a, hipStream_t s);
 hipError_t launch_key_setup(const uint8_t *keys, uint32_t key_len, uint32_t n_keys, const uint8_t *sbox,

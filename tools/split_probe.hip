@@ -151,7 +151,7 @@ int main() {
         }
         printf("%-44s %.4f ms  (%.3f Gpkt/s)\n", name, best, n / best / 1e6);
     };
-    timeit("fused k_encrypt", [&] { CHECK(launch_encrypt(a, 14, ncu, 0)); });
+    timeit("fused k_encrypt", [&] { CHECK(launch_encrypt(a, 14, ncu, nullptr, 0)); });
     timeit("AES-only (1024 thr x CUs)", [&] {
         hipLaunchKernelGGL(k_aes_only, dim3(ncu), dim3(1024), 131072, 0, rec, dsb, dpt, L, div, dtok2, tl, 0, n);
     });

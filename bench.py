@@ -296,7 +296,7 @@ def traffic_from_profiles(kernel, n, L, keys):
     return None
 
 
-def e2e_rate(ks, pt_dev, iv_dev, L, tl, n, stream, reps=3, chunks=16, n_streams=3):
+def e2e_rate(ks, pt_dev, iv_dev, L, tl, n, stream, reps=3, chunks=32, n_streams=3):
     """Host memory in, host memory out, pinned buffers:
     * serial: H2D of plaintext + IVs, encrypt, D2H of the tokens, one stream
       (and the mirror for decrypt: H2D of the tokens, decrypt, D2H);

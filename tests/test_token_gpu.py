@@ -213,6 +213,42 @@ def test_device_uniform_per_packet_keys(rt):
     assert np.array_equal(ref.reshape(len(sel), tl), tok.cpu().numpy()[sel])
 
 
+@pytest.mark.parametrize("n, n_keys", [(300_001, 1), (200_003, 4096)])
+def test_ragged_uniform_batch_chunk_loop(rt, n, n_keys):
+    """A uniform batch that does not divide over the persistent grid's lanes
+    (more than one pass, ragged last pass) runs the dynamic chunk loop: every
+    packet is encrypted exactly once (round trip of all n) and a seeded sample
+    is bit-exact vs the oracle, for one key and for per-packet keys."""
+    import torch
+    from reticulum_amd import device
+    L = 100
+    tl = rt.token_len(L)
+    rng = np.random.Generator(np.random.PCG64(n))
+    keys = rng.integers(0, 256, (n_keys, 64), dtype=np.uint8)
+    ks = rt.KeySet(keys if n_keys > 1 else keys[0].tobytes())
+    kidx = rng.integers(0, n_keys, n).astype(np.int32)
+    pt_h = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    iv_h = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    pt, iv = torch.from_numpy(pt_h).cuda(), torch.from_numpy(iv_h).cuda()
+    ki = torch.from_numpy(kidx).cuda() if n_keys > 1 else None
+    tok = torch.zeros((n, tl), dtype=torch.uint8, device="cuda")
+    for _ in range(2):          # the second launch takes another counter slot
+        device.encrypt_uniform(ks, pt, L, iv, tok, key_idx=ki)
+    back = torch.empty((n, tl - 48), dtype=torch.uint8, device="cuda")
+    out_len = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    status = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    device.decrypt_uniform(ks, tok, tl, back, out_len, status, key_idx=ki)
+    torch.cuda.synchronize()
+    assert int(status.abs().sum()) == 0
+    assert bool((out_len == L).all())
+    assert torch.equal(back[:, :L], pt)
+    sel = np.concatenate([np.arange(0, n, 211), np.arange(n - 64, n)])
+    ref, _, _ = _oracle_tokens(keys, pt_h[sel].reshape(-1), np.arange(len(sel), dtype=np.uint64) * L,
+                               np.full(len(sel), L, np.uint32), iv_h[sel],
+                               kidx[sel].astype(np.uint32) if n_keys > 1 else None)
+    assert np.array_equal(ref.reshape(len(sel), tl), tok.cpu().numpy()[sel])
+
+
 def test_resource_chunks_16k(rt):
     """Config c4 shape (Resource-sized 16 KiB tokens), reduced count."""
     import torch

@@ -204,6 +204,7 @@ def main():
     dom = "decrypt" if dec_avg > enc_avg else "encrypt"
     dom_ms = max(enc_avg, dec_avg)
     dom_ops = ops_d if dom == "decrypt" else ops_e
+    traffic = traffic_from_profiles(dom, n, L, args.keys)
     achieved = dom_ops / (dom_ms * 1e-3)
     bytes_enc = n * (L + 16 + tl + 0)         # read pt + iv, write token
     bytes_dec = n * (tl + (tl - 48) + 8)      # read token, write pt + len + status
@@ -250,17 +251,23 @@ def main():
         },
         "roofline": {"bound": "valu", "kernel": dom, "achieved": achieved / 1e12, "peak": peak_valu / 1e12,
                      "unit": "TOP/s", "frac": achieved / peak_valu,
-                     "traffic": traffic_from_profiles(dom, n, L, args.keys),
+                     "traffic": (traffic or {}).get("bytes_with_x2_fetch_correction"),
+                     "traffic_detail": traffic,
                      "ops_per_packet": ops_dec(L) if dom == "decrypt" else ops_enc(L),
                      "algorithmic_bytes_per_launch": hbm_bytes,
                      "algorithmic_hbm_gb_s": hbm_bytes / (dom_ms * 1e-3) / 1e9,
                      "frac_of_survey_P": achieved / (n_cu * 64 * 2.4e9),
+                     "measured_valu_peak": n_cu * 4 * 64 / 2.74 * 2.4e9 / 1e12,
+                     "frac_of_measured_valu_peak": achieved / (n_cu * 4 * 64 / 2.74 * 2.4e9),
+                     "sustained_clock_ghz": sustained_clock_ghz(dom, n, L, args.keys),
                      "lds_frac": n * blocks(L) * LDS_LOOKUPS_PER_BLOCK / (dom_ms * 1e-3) / peak_lds,
                      "note": "achieved = canonical int32 VALU lane-ops per launch (SURVEY §8(d): 352/AES block, "
                              "1464/SHA-256 compression, +8 tag compare) / HIP-event kernel time; peak = CUs x 128 "
-                             "lanes x 2.4 GHz (full-rate VALU); frac_of_survey_P uses BASELINE.md §5's P = CUs x 64 "
+                             "lanes x 2.4 GHz (full-rate VALU); measured_valu_peak = v_xor_b32 at 2.74 cycles per wave64 "
+                             "instruction per SIMD (tools/valu_peak.hip, DESIGN.md 4.5); sustained_clock_ghz from the "
+                             "committed PMC run (GRBM_GUI_ACTIVE / 8 XCDs / kernel-trace average); frac_of_survey_P uses BASELINE.md §5's P = CUs x 64 "
                              "x 2.4 GHz; traffic = HBM bytes per launch from the committed rocprofv3 PMC summary "
-                             "(profiles/*_pmc.json; see traffic.calibration). On gfx950 LDS lookups and VALU issue do not "
+                             "(profiles/*_pmc.json, FETCH_SIZE x 2 + WRITE_SIZE; see traffic_detail.calibration). On gfx950 LDS lookups and VALU issue do not "
                              "overlap (tools/overlap_probe.hip: their times add), so the kernel's floor is the LDS time "
                              "plus the VALU time of its instruction mix (DESIGN.md §4.5)"},
         "cpu_baseline": cpu,
@@ -271,12 +278,9 @@ def main():
         dist.destroy_process_group()
 
 
-def traffic_from_profiles(kernel, n, L, keys):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    whose workload matches (profiles/<round>_pmc.json, tools/pmc_summary.py)."""
+def _newest_pmc(kernel, n, L, keys):
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
-    for path in reversed(files):
+    for path in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))):
         try:
             with open(path) as f:
                 d = json.load(f)
@@ -284,15 +288,44 @@ def traffic_from_profiles(kernel, n, L, keys):
             continue
         meta = d.get("_workload", {})
         if meta.get("packets") == n and meta.get("length") == L and meta.get("keys") == keys and kernel in d:
-            raw = d[kernel].get("hbm_bytes_per_launch_uncorrected")
-            if raw:
-                return {"bytes": raw, "bytes_with_x2_fetch_correction": d[kernel].get("hbm_bytes_per_launch"),
-                        "source": os.path.relpath(path, ROOT),
-                        "calibration": "FETCH_SIZE + WRITE_SIZE as counted. The guide's x2 FETCH correction is for "
-                                       "coalesced 16-B streams (our control reads 0.50x its known bytes); on this "
-                                       "kernel's 500-B-stride lane pattern a pure read of a known 524 MB reports 1.40x "
-                                       "(tools/fetch_calib.hip, profiles/r01c_fetch_calib.txt), the encrypt kernel "
-                                       "1.32x of its algorithmic reads: no over-fetch beyond the access pattern's own"}
+            return path, d
+    return None, None
+
+
+def sustained_clock_ghz(kernel, n, L, keys):
+    """Shader clock under this load: GRBM_GUI_ACTIVE per launch (summed over
+    the 8 XCDs) / 8 over the kernel's average duration in the kernel trace of
+    the same profiling run (profiles/<round>_kernel_stats.csv)."""
+    import csv
+    path, d = _newest_pmc(kernel, n, L, keys)
+    if not path:
+        return None
+    stats = path.replace("_pmc.json", "_kernel_stats.csv")
+    tag = "k_encrypt<14, " if kernel == "encrypt" else "k_decrypt<14, "
+    try:
+        with open(stats) as f:
+            rows = [r for r in csv.DictReader(f) if tag in r["Name"]]
+        ns = float(rows[0]["AverageNs"])
+        return d[kernel]["GRBM_GUI_ACTIVE"] / 8 / ns
+    except (OSError, KeyError, IndexError, ValueError):
+        return None
+
+
+def traffic_from_profiles(kernel, n, L, keys):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    whose workload matches (profiles/<round>_pmc.json, tools/pmc_summary.py)."""
+    path, d = _newest_pmc(kernel, n, L, keys)
+    if path:
+        raw = d[kernel].get("hbm_bytes_per_launch_uncorrected")
+        if raw:
+            return {"bytes": raw, "bytes_with_x2_fetch_correction": d[kernel].get("hbm_bytes_per_launch"),
+                    "source": os.path.relpath(path, ROOT),
+                    "calibration": "roofline.traffic = FETCH_SIZE x 2 + WRITE_SIZE (the guide's gfx950 correction); bytes = "
+                                   "FETCH_SIZE + WRITE_SIZE as counted. The x2 FETCH correction is for "
+                                   "coalesced 16-B streams (our control reads 0.50x its known bytes); on this "
+                                   "kernel's 500-B-stride lane pattern a pure read of a known 524 MB reports 1.40x "
+                                   "(tools/fetch_calib.hip, profiles/r01c_fetch_calib.txt), the encrypt kernel "
+                                   "1.32x of its algorithmic reads: no over-fetch beyond the access pattern's own"}
     return None
 
 

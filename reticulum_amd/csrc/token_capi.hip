@@ -11,6 +11,7 @@
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/rnstok.h"
 #include "token_device.h"
@@ -32,7 +33,49 @@ struct rt_ctx {
     static constexpr uint32_t QUEUE_SLOTS = 1024;
     uint32_t *d_queues = nullptr;
     std::atomic<uint32_t> q_next{0};
+    // Key-record buffers of destroyed key sets, kept for the next key set of
+    // a similar size: per-packet keying (a fresh HKDF key set per batch,
+    // Identity.py:837-846) would otherwise pay a hipMalloc of n x 544 B per
+    // batch on the host timeline.  Destroy already synchronises the device, so
+    // a cached buffer is idle.
+    std::mutex rec_mu;
+    std::vector<std::pair<uint64_t, uint32_t *>> rec_cache;   // (capacity bytes, buffer)
 };
+
+static constexpr size_t REC_CACHE_MAX = 4;
+
+static uint32_t *rec_alloc(rt_ctx *c, uint64_t bytes, uint64_t *cap) {
+    {
+        std::lock_guard<std::mutex> g(c->rec_mu);
+        for (size_t i = 0; i < c->rec_cache.size(); ++i) {
+            const uint64_t have = c->rec_cache[i].first;
+            if (have >= bytes && have <= 2 * bytes + (1u << 20)) {
+                uint32_t *p = c->rec_cache[i].second;
+                *cap = have;
+                c->rec_cache.erase(c->rec_cache.begin() + i);
+                return p;
+            }
+        }
+    }
+    uint32_t *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    *cap = bytes;
+    return p;
+}
+
+static void rec_release(rt_ctx *c, uint32_t *p, uint64_t cap) {
+    if (!p) return;
+    uint32_t *evict = nullptr;
+    {
+        std::lock_guard<std::mutex> g(c->rec_mu);
+        c->rec_cache.emplace_back(cap, p);
+        if (c->rec_cache.size() > REC_CACHE_MAX) {
+            evict = c->rec_cache.front().second;
+            c->rec_cache.erase(c->rec_cache.begin());
+        }
+    }
+    if (evict) hipFree(evict);
+}
 
 static uint32_t *next_queue(rt_ctx *c) {
     return c->d_queues ? c->d_queues + 16u * (c->q_next.fetch_add(1) % rt_ctx::QUEUE_SLOTS) : nullptr;
@@ -43,6 +86,7 @@ struct rt_keyset {
     uint32_t key_len = 0, n_keys = 0;
     int nr = 0;
     uint32_t *d_rec = nullptr;
+    uint64_t rec_cap = 0;          // bytes of d_rec (it may come from the context's cache)
 };
 
 static thread_local std::string g_err;
@@ -141,6 +185,7 @@ void rt_destroy(rt_ctx *c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     hipFree(c->d_sbox);
     hipFree(c->d_queues);
+    for (auto &e : c->rec_cache) hipFree(e.second);
     hipFree(c->d_work);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -167,7 +212,7 @@ rt_keyset *rt_keyset_create_device(rt_ctx *c, const uint8_t *d_keys, uint32_t ke
     k->n_keys = n_keys;
     k->nr = key_len == 64 ? 14 : 10;
     hipStream_t s = pick(c, stream);
-    if (hipMalloc(&k->d_rec, (uint64_t)n_keys * REC_WORDS * 4) != hipSuccess) {
+    if (!(k->d_rec = rec_alloc(c, (uint64_t)n_keys * REC_WORDS * 4, &k->rec_cap))) {
         fail(RT_E_NOMEM, "key table allocation failed");
         delete k;
         return nullptr;
@@ -207,7 +252,7 @@ void rt_keyset_destroy(rt_keyset *k) {
     if (!k) return;
     hipSetDevice(k->ctx->device);
     hipDeviceSynchronize();
-    hipFree(k->d_rec);
+    rec_release(k->ctx, k->d_rec, k->rec_cap);
     delete k;
 }
 

@@ -85,27 +85,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_add(uint64_t *out, const ui
     if (total_out && i == 0) *total_out = part[(n + SCAN_BLOCK - 1) / SCAN_BLOCK];
 }
 
-// ---------------------------------------------------- wave-level helpers --
-//
-// The framing kernels give each packet (frame) to one wave: its lanes cover
-// 4 consecutive bytes each of a 256-byte window, so loads and stores are
-// contiguous across the wave; escapes are found with byte-parallel compares
-// and output positions with a wave prefix sum.
+// ------------------------------------------------------- byte helpers --
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-    const uint32_t l = threadIdx.x & 63u;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (l >= (uint32_t)d) x += y;
-    }
-    return x;
-}
-__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
-    return x;
-}
 // little-endian word of p[i, i+4), bytes at or past `end` read as 0
 __device__ __forceinline__ uint32_t ld4_upto(const uint8_t *p, uint64_t i, uint64_t end) {
     if (i + 4 <= end) {
@@ -118,7 +99,6 @@ __device__ __forceinline__ uint32_t ld4_upto(const uint8_t *p, uint64_t i, uint6
         if (i + k < end) v |= (uint32_t)p[i + k] << (8 * k);
     return v;
 }
-__device__ __forceinline__ void st4u(uint8_t *p, uint32_t v) { __builtin_memcpy(p, &v, 4); }
 // 0x80 in every byte of x equal to the byte replicated in c4 (exact: no borrow crosses bytes)
 __device__ __forceinline__ uint32_t eqbytes(uint32_t x, uint32_t c4) {
     const uint32_t t = x ^ c4;
@@ -127,46 +107,90 @@ __device__ __forceinline__ uint32_t eqbytes(uint32_t x, uint32_t c4) {
 __device__ __forceinline__ uint32_t escbytes(uint32_t x) { return eqbytes(x, 0x7E7E7E7Eu) | eqbytes(x, 0x7D7D7D7Du); }
 
 // ------------------------------------------------------------- framing --
+//
+// One DPP row (16 lanes) per packet, 4 packets per wave: lane r of the row
+// covers bytes [16r, 16r+16) of a 256-byte window with one 16-B load, so a
+// wave keeps 4 packets' loads in flight (one wave per packet with 4-B lanes
+// held one 500-B packet per wave and ran at 1.7-2.1 TB/s, latency-bound).
+// Row sums and row prefix sums are DPP row_ror / row_shr adds.
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+// every lane of the 16-lane row gets the row's total
+__device__ __forceinline__ uint32_t row_sum16(uint32_t x) {
+    x += dpp<0x128>(x);     // row_ror:8
+    x += dpp<0x124>(x);     // row_ror:4
+    x += dpp<0x122>(x);     // row_ror:2
+    x += dpp<0x121>(x);     // row_ror:1
+    return x;
+}
+// inclusive prefix sum within the 16-lane row (row_shr reads 0 past the row start)
+__device__ __forceinline__ uint32_t row_incl_scan16(uint32_t x) {
+    x += dpp<0x111>(x);     // row_shr:1
+    x += dpp<0x112>(x);     // row_shr:2
+    x += dpp<0x114>(x);     // row_shr:4
+    x += dpp<0x118>(x);     // row_shr:8
+    return x;
+}
+// 16 bytes of p[i, i+16), bytes at or past `end` read as 0
+__device__ __forceinline__ u32x4 ld16_upto(const uint8_t *p, uint64_t i, uint64_t end) {
+    if (i + 16 <= end) return ld16(p + i);
+    u32x4 v = {ld4_upto(p, i, end), ld4_upto(p, i + 4, end), ld4_upto(p, i + 8, end), ld4_upto(p, i + 12, end)};
+    return v;
+}
+__device__ __forceinline__ uint32_t esc_count16(u32x4 v) {
+    return __builtin_popcount(escbytes(v.x)) + __builtin_popcount(escbytes(v.y)) + __builtin_popcount(escbytes(v.z)) +
+           __builtin_popcount(escbytes(v.w));
+}
 
 __global__ __launch_bounds__(256) void k_hdlc_count(const uint8_t *pkt, const uint64_t *off, const uint32_t *len,
                                                     uint64_t *flen, uint32_t n) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t i = w0; i < n; i += nw) {
-        const uint8_t *p = pkt + off[i];
-        const uint32_t L = len[i];
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & 15u;
+    const uint32_t g0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, ng = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t g = g0; 4ull * g < n; g += ng) {
+        const uint32_t i = 4u * g + (lane >> 4);
+        const bool valid = i < n;
+        const uint8_t *p = pkt + (valid ? off[i] : 0);
+        const uint32_t L = valid ? len[i] : 0u;
         uint32_t extra = 0;
-        for (uint32_t b = 4u * lane; b < L; b += 256u) extra += __builtin_popcount(escbytes(ld4_upto(p, b, L)));
-        extra = wave_sum(extra);
-        if (lane == 0) flen[i] = 2ull + L + extra;     // 7E || escape(p) || 7E
+        for (uint32_t b = 16u * rl; b < L; b += 256u) extra += esc_count16(ld16_upto(p, b, L));
+        extra = row_sum16(extra);
+        if (rl == 0 && valid) flen[i] = 2ull + L + extra;     // 7E || escape(p) || 7E
     }
 }
 
 __global__ __launch_bounds__(256) void k_hdlc_write(const uint8_t *pkt, const uint64_t *off, const uint32_t *len,
                                                     const uint64_t *foff, uint8_t *out, uint32_t n) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t i = w0; i < n; i += nw) {
-        const uint8_t *p = pkt + off[i];
-        uint8_t *o = out + foff[i];
-        const uint32_t L = len[i];
-        if (lane == 0) o[0] = FLAG;
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & 15u;
+    const uint32_t g0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, ng = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t g = g0; 4ull * g < n; g += ng) {
+        const uint32_t i = 4u * g + (lane >> 4);
+        const bool valid = i < n;
+        const uint8_t *p = pkt + (valid ? off[i] : 0);
+        uint8_t *o = out + (valid ? foff[i] : 0);
+        const uint32_t L = valid ? len[i] : 0u;
+        if (rl == 0 && valid) o[0] = FLAG;
         uint64_t base = 1;                       // output position of the window's first byte
+        // rows run as many windows as their own packet needs; the DPP ops
+        // below read only lanes of the same row, which share the trip count
         for (uint32_t w = 0; w < L; w += 256u) {
-            const uint32_t b = w + 4u * lane;
-            const uint32_t nb = b < L ? min(4u, L - b) : 0u;
-            const uint32_t x = nb ? ld4_upto(p, b, L) : 0u;
-            const uint32_t esc = __builtin_popcount(escbytes(x));
+            const uint32_t b = w + 16u * rl;
+            const uint32_t nb = b < L ? min(16u, L - b) : 0u;
+            const u32x4 v = nb ? ld16_upto(p, b, L) : u32x4{0u, 0u, 0u, 0u};
+            const uint32_t esc = esc_count16(v);
             const uint32_t sz = nb + esc;
-            const uint32_t incl = wave_incl_scan(sz);
+            const uint32_t incl = row_incl_scan16(sz);
             uint8_t *q = o + base + (incl - sz);
-            if (esc == 0 && nb == 4) {
-                st4u(q, x);
+            if (esc == 0 && nb == 16) {
+                st16(q, v);
             } else {
                 // HDLC.escape: ESC first, then FLAG (TCPInterface.py:50-52); per byte the same
+                const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
                 uint32_t wpos = 0;
                 for (uint32_t k = 0; k < nb; ++k) {
-                    const uint8_t c = (uint8_t)(x >> (8 * k));
+                    const uint8_t c = (uint8_t)(wv[k >> 2] >> (8 * (k & 3)));
                     if (c == ESC || c == FLAG) {
                         q[wpos++] = ESC;
                         q[wpos++] = c ^ ESC_MASK;
@@ -175,39 +199,54 @@ __global__ __launch_bounds__(256) void k_hdlc_write(const uint8_t *pkt, const ui
                     }
                 }
             }
-            base += __shfl(incl, 63, 64);
+            base += row_sum16(sz);
         }
-        if (lane == 0) o[base] = FLAG;
+        if (rl == 0 && valid) o[base] = FLAG;
     }
 }
 
 // ----------------------------------------------------------- deframing --
 
-constexpr uint32_t FLAG_CHUNK = 4096;        // stream bytes per workgroup (256 threads x 16)
+constexpr uint32_t FLAG_CHUNK = 16384;       // stream bytes per workgroup (256 threads x 64)
 
+// 0x80 per byte of the four words equal to c4
+__device__ __forceinline__ uint32_t flags16(u32x4 v) {
+    return __builtin_popcount(eqbytes(v.x, 0x7E7E7E7Eu)) + __builtin_popcount(eqbytes(v.y, 0x7E7E7E7Eu)) +
+           __builtin_popcount(eqbytes(v.z, 0x7E7E7E7Eu)) + __builtin_popcount(eqbytes(v.w, 0x7E7E7E7Eu));
+}
+
+// flags per chunk; each load instruction covers 1 KiB contiguous across the
+// workgroup's threads (the count does not depend on the order)
 __global__ __launch_bounds__(256) void k_flag_count(const uint8_t *buf, uint64_t len, uint64_t *cnt) {
     const uint64_t base = (uint64_t)blockIdx.x * FLAG_CHUNK + threadIdx.x * 16ull;
     uint32_t c = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < 16; k += 4)
-        if (base + k < len) c += __builtin_popcount(eqbytes(ld4_upto(buf, base + k, len), 0x7E7E7E7Eu));
+    for (uint32_t k = 0; k < FLAG_CHUNK / 4096u; ++k) {
+        const uint64_t q = base + 4096ull * k;
+        if (q < len) c += flags16(ld16_upto(buf, q, len));
+    }
+    c = row_sum16(c);
     __shared__ uint32_t s;
     if (threadIdx.x == 0) s = 0;
     __syncthreads();
-    atomicAdd(&s, c);
+    if ((threadIdx.x & 15u) == 0) atomicAdd(&s, c);
     __syncthreads();
     if (threadIdx.x == 0) cnt[blockIdx.x] = s;
 }
 
+// flag positions in stream order: thread t owns bytes [64t, 64t+64) of its chunk
 __global__ __launch_bounds__(256) void k_flag_scatter(const uint8_t *buf, uint64_t len, const uint64_t *cnt_off,
                                                       uint64_t *pos) {
-    const uint64_t base = (uint64_t)blockIdx.x * FLAG_CHUNK + threadIdx.x * 16ull;
-    uint32_t m[4], c = 0;
+    const uint64_t base = (uint64_t)blockIdx.x * FLAG_CHUNK + threadIdx.x * 64ull;
+    uint32_t m[16], c = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
-        m[k] = base + 4 * k < len ? eqbytes(ld4_upto(buf, base + 4 * k, len), 0x7E7E7E7Eu) : 0u;
-        c += __builtin_popcount(m[k]);
+        const u32x4 v = base + 16 * k < len ? ld16_upto(buf, base + 16 * k, len) : u32x4{0u, 0u, 0u, 0u};
+        m[4 * k] = eqbytes(v.x, 0x7E7E7E7Eu); m[4 * k + 1] = eqbytes(v.y, 0x7E7E7E7Eu);
+        m[4 * k + 2] = eqbytes(v.z, 0x7E7E7E7Eu); m[4 * k + 3] = eqbytes(v.w, 0x7E7E7E7Eu);
     }
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) c += __builtin_popcount(m[k]);
     // in-order rank of this thread's flags inside the chunk
     __shared__ uint32_t sh[256];
     sh[threadIdx.x] = c;
@@ -218,20 +257,23 @@ __global__ __launch_bounds__(256) void k_flag_scatter(const uint8_t *buf, uint64
         sh[threadIdx.x] += add;
         __syncthreads();
     }
+    if (c == 0) return;
     uint64_t w = cnt_off[blockIdx.x] + sh[threadIdx.x] - c;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k)
+    for (uint32_t k = 0; k < 16; ++k)
         for (uint32_t f = m[k]; f; f &= f - 1) pos[w++] = base + 4 * k + (__builtin_ctz(f) >> 3);
 }
 
-// One wave per consecutive flag pair (k, k+1): the read loop's frame
-// buf[pos_k+1 : pos_{k+1}) with its two bytes.replace passes (TCPInterface.py:
-// 397-398: ESC,5E -> 7E first, then ESC,5D -> 7D, each left to right and
-// non-overlapping), written at out + pos_k + 1.  Neither pattern can overlap
-// itself and a 7D is never the byte a replacement removes, so the two passes
-// are one local rule: byte i is dropped when byte i-1 is 7D and byte i is 5E
-// or 5D; a kept 7D followed by 5E becomes 7E.  Kept bytes are placed with a
-// wave prefix sum.
+// One DPP row (16 lanes x 16 B) per consecutive flag pair (k, k+1), 4 pairs
+// per wave: the read loop's frame buf[pos_k+1 : pos_{k+1}) with its two
+// bytes.replace passes (TCPInterface.py:397-398: ESC,5E -> 7E first, then
+// ESC,5D -> 7D, each left to right and non-overlapping), written at
+// out + pos_k + 1.  Neither pattern can overlap itself and a 7D is never the
+// byte a replacement removes, so the two passes are one local rule on the
+// input bytes: byte i is dropped when byte i-1 is 7D and byte i is 5E or 5D;
+// a 7D followed by 5E becomes 7E.  Evaluated on whole words (eqbytes on the
+// words shifted by one byte); the byte before a frame is its opening flag and
+// the byte after it the closing flag, so neither rule fires across the frame
+// edge.  Kept bytes are placed with a row prefix sum.
 __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, const uint64_t *pos, const uint64_t *nflags_p,
                                                        uint64_t max_pairs, uint32_t hw_mtu, uint32_t ifac_size,
                                                        uint8_t *out, uint64_t *frame_off, uint32_t *frame_len,
@@ -239,45 +281,48 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, const
     const uint64_t nf = *nflags_p;
     uint64_t npairs = nf > 1 ? nf - 1 : 0;
     if (npairs > max_pairs) npairs = max_pairs;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t k = w0; k < npairs; k += nw) {
-        const uint64_t a = pos[k] + 1, e = pos[k + 1];
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & 15u;
+    const uint64_t g0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, ng = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t g = g0; 4 * g < npairs; g += ng) {
+        const uint64_t k = 4 * g + (lane >> 4);
+        const bool valid = k < npairs;
+        const uint64_t a = valid ? pos[k] + 1 : 0, e = valid ? pos[k + 1] : 0;
         uint8_t *o = out + a;
         uint64_t kept_total = 0;
-        uint32_t carry = 0;                       // last byte of the previous window
+        uint32_t carry = FLAG;                    // the byte before the window: the opening flag first
         for (uint64_t w = a; w < e; w += 256u) {
-            const uint64_t b = w + 4u * lane;
-            const uint32_t nb = b < e ? (uint32_t)min((uint64_t)4, e - b) : 0u;
-            const uint32_t x = nb ? ld4_upto(buf, b, e) : 0u;
-            uint32_t prevb = __shfl_up(x, 1, 64) >> 24;
-            if (lane == 0) prevb = carry;
-            uint32_t nextb = __shfl_down(x, 1, 64) & 0xFFu;
-            if (lane == 63) nextb = b + 4 < e ? buf[b + 4] : 0u;
-            uint32_t outw = 0, kept = 0;
-            for (uint32_t j = 0; j < nb; ++j) {
-                const uint32_t c = (x >> (8 * j)) & 0xFFu;
-                const uint32_t pc = j ? (x >> (8 * (j - 1))) & 0xFFu : prevb;
-                const uint32_t nc = j < 3 ? (x >> (8 * (j + 1))) & 0xFFu : nextb;
-                const bool has_prev = b + j > a, has_next = b + j + 1 < e;
-                const bool drop = has_prev && pc == ESC && (c == (FLAG ^ ESC_MASK) || c == (ESC ^ ESC_MASK));
-                if (!drop) {
-                    const uint32_t v = (c == ESC && has_next && nc == (FLAG ^ ESC_MASK)) ? FLAG : c;
-                    outw |= v << (8 * kept);
-                    ++kept;
-                }
+            const uint64_t b = w + 16u * rl;
+            const uint32_t nb = b < e ? (uint32_t)min((uint64_t)16, e - b) : 0u;
+            const u32x4 v = nb ? ld16_upto(buf, b, e) : u32x4{0u, 0u, 0u, 0u};
+            uint32_t prevb = dpp<0x111>(v.w) >> 24;          // row_shr:1: the previous lane's last byte
+            if (rl == 0) prevb = carry;
+            uint32_t nextb = dpp<0x101>(v.x) & 0xFFu;         // row_shl:1: the next lane's first byte
+            if (rl == 15) nextb = b + 16 < e ? buf[b + 16] : 0u;
+            const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+            uint32_t y[4], drop[4], ndrop = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t pw = __builtin_amdgcn_alignbit(x[j], j ? x[j - 1] : prevb << 24, 24);   // previous bytes
+                const uint32_t nw = __builtin_amdgcn_alignbit(j < 3 ? x[j + 1] : nextb, x[j], 8);      // next bytes
+                drop[j] = eqbytes(pw, 0x7D7D7D7Du) & (eqbytes(x[j], 0x5E5E5E5Eu) | eqbytes(x[j], 0x5D5D5D5Du));
+                const uint32_t conv = eqbytes(x[j], 0x7D7D7D7Du) & eqbytes(nw, 0x5E5E5E5Eu);
+                y[j] = x[j] ^ ((conv >> 7) * 3u);                                                     // 7D -> 7E
+                ndrop += __builtin_popcount(drop[j]);
             }
-            const uint32_t incl = wave_incl_scan(kept);
+            const uint32_t kept = nb - ndrop;
+            const uint32_t incl = row_incl_scan16(kept);
             uint8_t *q = o + kept_total + (incl - kept);
-            if (kept == 4) {
-                st4u(q, outw);
+            if (ndrop == 0 && nb == 16) {
+                st16(q, u32x4{y[0], y[1], y[2], y[3]});
             } else {
-                for (uint32_t t = 0; t < kept; ++t) q[t] = (uint8_t)(outw >> (8 * t));
+                uint32_t t = 0;
+                for (uint32_t j = 0; j < nb; ++j)
+                    if (!((drop[j >> 2] >> (8 * (j & 3) + 7)) & 1u)) q[t++] = (uint8_t)(y[j >> 2] >> (8 * (j & 3)));
             }
-            kept_total += __shfl(incl, 63, 64);
-            carry = __shfl(x, 63, 64) >> 24;
+            kept_total += row_sum16(kept);
+            carry = row_sum16(rl == 15 ? v.w >> 24 : 0u);      // the window's last byte, to every lane
         }
-        if (lane == 0) {
+        if (rl == 0 && valid) {
             frame_off[k] = a;
             frame_len[k] = (uint32_t)kept_total;
             // check_frame_len (TCPInterface.py:336-339); empty frames are skipped (:400)
@@ -569,8 +614,8 @@ hipError_t launch_hdlc_frame(const uint8_t *pkt, const uint64_t *off, const uint
     if (n == 0) return hipSuccess;
     uint64_t *flen = (uint64_t *)ws;
     uint64_t *part = flen + n;
-    // one wave per packet, grid-stride: 4 packets per 256-thread workgroup
-    const unsigned g = (unsigned)min((uint64_t)(n + 3) / 4, (uint64_t)WAVE_GRID);
+    // one DPP row per packet: 16 packets per 256-thread workgroup, grid-stride
+    const unsigned g = (unsigned)min((uint64_t)(n + 15) / 16, (uint64_t)WAVE_GRID);
     hipLaunchKernelGGL(k_hdlc_count, dim3(g), dim3(256), 0, s, pkt, off, len, flen, n);
     hipError_t e = launch_scan(flen, frame_off, n, part, frame_off + n, s);
     if (e != hipSuccess) return e;
@@ -602,7 +647,7 @@ hipError_t launch_hdlc_deframe(const uint8_t *buf, uint64_t len, uint32_t hw_mtu
     hipLaunchKernelGGL(k_deframe_counts, dim3(1), dim3(1), 0, s, nflags, pos, len, hw_mtu, counts);
     // the pair count lives on the device: a grid-stride kernel sized by the caller's capacity
     if (max_pairs) {
-        const uint64_t g = min((max_pairs + 3) / 4, (uint64_t)WAVE_GRID);     // one wave per frame
+        const uint64_t g = min((max_pairs + 15) / 16, (uint64_t)WAVE_GRID);   // one DPP row per frame
         hipLaunchKernelGGL(k_hdlc_unescape, dim3((unsigned)g), dim3(256), 0, s, buf, pos, nflags, max_pairs, hw_mtu,
                            ifac_size, out, frame_off, frame_len, status);
     }

@@ -383,6 +383,18 @@ __device__ __forceinline__ void key_midstates(const uint8_t *key, uint32_t klen,
 // IFAC, reassembled [un0 & 0x7f, un1] || un[2+n:] (Transport.py:1441-1475).
 template <bool MASK>
 __global__ __launch_bounds__(256) void k_ifac(IfacArgs a) {
+    // the ifac_key midstates are the same for every packet: wave 0 computes
+    // them once per workgroup (2 of a 500-B packet's 38 compressions)
+    __shared__ uint32_t key_ms[16];
+    if (threadIdx.x < 64u) {
+        uint32_t ki[8], ko[8];
+        key_midstates(a.ifac_key, a.key_len, ki, ko);
+        if (threadIdx.x == 0u) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) { key_ms[k] = ki[k]; key_ms[8 + k] = ko[k]; }
+        }
+    }
+    __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
     const uint8_t *raw = a.pkt + a.pkt_off[i];
@@ -403,7 +415,8 @@ __global__ __launch_bounds__(256) void k_ifac(IfacArgs a) {
     // HKDF (HKDF.py:35-62) with salt = ifac_key, ikm = ifac, no context:
     // PRK = HMAC(ifac_key, ifac); T_b = HMAC(PRK, T_{b-1} || b+1)
     uint32_t hi[8], ho[8], prk[8];
-    key_midstates(a.ifac_key, a.key_len, hi, ho);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { hi[k] = key_ms[k]; ho[k] = key_ms[8 + k]; }
     {
         uint32_t w[16], h[8];
         // ifac_size <= 64: one or two message blocks after the ipad block

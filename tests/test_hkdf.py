@@ -150,3 +150,33 @@ def test_gpu_derived_keyset_per_packet_tokens(key_len):
     for i in range(0, n, 61):
         key = ctoken.hkdf(key_len, ikm[i].tobytes(), salt[i].tobytes())
         assert th[i].tobytes() == ctoken.encrypt(key, iv[i].tobytes(), pt[i].tobytes()), i
+
+
+@pytest.mark.gpu
+def test_gpu_keyset_record_buffer_reuse():
+    """Per-batch key sets: destroying a key set returns its record buffer to
+    the context's cache and the next key set of a similar size reuses it.
+    Every reused set must be fully rewritten: tokens of batch k match the
+    oracle under batch k's own keys (never a previous batch's), for sizes
+    that hit the cache (equal, slightly smaller) and one that does not."""
+    import gc
+    import torch
+    from reticulum_amd import device
+    L = 100
+    tl = rt.token_len(L)
+    for step, n in enumerate([3000, 3000, 2900, 3000, 700, 3000]):
+        rng = np.random.Generator(np.random.PCG64(100 + step))
+        ikm = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        salt = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+        ks = device.derive_keyset(torch.from_numpy(ikm).cuda(), torch.from_numpy(salt).cuda(), key_len=64)
+        pt = rng.integers(0, 256, (n, L), dtype=np.uint8)
+        iv = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+        tok = torch.empty((n, tl), dtype=torch.uint8, device="cuda")
+        device.encrypt_uniform(ks, torch.from_numpy(pt).cuda(), L, torch.from_numpy(iv).cuda(), tok,
+                               key_idx=torch.arange(n, dtype=torch.int32, device="cuda"))
+        th = tok.cpu().numpy()
+        for i in list(range(0, n, 97)) + [n - 1]:
+            key = ctoken.hkdf(64, ikm[i].tobytes(), salt[i].tobytes())
+            assert th[i].tobytes() == ctoken.encrypt(key, iv[i].tobytes(), pt[i].tobytes()), (step, i)
+        del ks
+        gc.collect()

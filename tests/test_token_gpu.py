@@ -315,6 +315,43 @@ def test_sorted_variable_batch_matches_unsorted_and_oracle(rt):
         assert bh[coff[i]:coff[i] + lens[i]].tobytes() == buf[off[i]:off[i] + lens[i]].tobytes()
 
 
+@pytest.mark.parametrize("n", [2, 63, 64, 65, 200])
+@pytest.mark.parametrize("n_keys", [1, 7])
+def test_sorted_small_batches_chunk_edges(rt, n, n_keys):
+    """Length-ordered launches around the 64-packet chunk size of the dynamic
+    packet loop (one partial chunk, exactly one, one plus one packet): the
+    tokens equal the oracle's and sorted decrypt restores every plaintext."""
+    import torch
+    from reticulum_amd import device
+    rng = np.random.Generator(np.random.PCG64(1000 + n + n_keys))
+    lens = rng.integers(0, 1200, n).astype(np.int32)
+    keys, buf, off, ulens, ivs, kidx = _random_batch(rng, n, lens, n_keys)
+    ks = rt.KeySet(keys if n_keys > 1 else keys[0].tobytes())
+    ref, toff, tl = _oracle_tokens(keys, buf, off, ulens, ivs, kidx)
+    cu = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    d_k = cu(kidx.astype(np.int32)) if kidx is not None else None
+    tok = torch.zeros(ref.size, dtype=torch.uint8, device="cuda")
+    device.encrypt(ks, cu(buf), cu(off.astype(np.int64)), cu(lens), cu(ivs), tok, cu(toff.astype(np.int64)),
+                   key_idx=d_k, sort=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(ref, tok.cpu().numpy())
+    cap = tl.astype(np.int64) - 48
+    coff = np.zeros(n, np.int64)
+    coff[1:] = np.cumsum(cap[:-1])
+    back = torch.zeros(int(cap.sum()), dtype=torch.uint8, device="cuda")
+    ol = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    device.decrypt(ks, tok, cu(toff.astype(np.int64)), cu(tl.astype(np.int32)), back, cu(coff), ol, st,
+                   key_idx=d_k, sort=True)
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0
+    assert np.array_equal(ol.cpu().numpy(), lens)
+    bh = back.cpu().numpy()
+    for i in range(n):
+        o, L = int(off[i]), int(lens[i])
+        assert bh[coff[i]:coff[i] + L].tobytes() == buf[o:o + L].tobytes()
+
+
 @pytest.mark.parametrize("n,L,klen", [(300, 1024, 64), (300, 1500, 64), (20000, 4095, 64), (2048, 16391, 64),
                                        (1, 1024, 64), (129, 1039, 64), (257, 1036, 64), (300, 2047, 32),
                                        (5000, 1055, 32), (64, 1064, 64)])

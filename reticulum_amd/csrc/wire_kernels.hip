@@ -28,7 +28,7 @@ namespace rnstok {
 
 namespace {
 
-constexpr uint8_t FLAG = 0x7E, ESC = 0x7D, ESC_MASK = 0x20;
+constexpr uint8_t FLAG = 0x7E;      // HDLC flag; escapes are 7D x^0x20 (eqbytes constants below)
 constexpr uint32_t HEADER_MINSIZE = 19, DST_LEN = 16, PATHFINDER_M = 128;
 constexpr uint32_t SCAN_BLOCK = 1024;
 constexpr uint32_t WAVE_GRID = 16384;        // workgroups of the wave-per-frame kernels (grid-stride beyond)
@@ -145,6 +145,54 @@ __device__ __forceinline__ uint32_t esc_count16(u32x4 v) {
            __builtin_popcount(escbytes(v.w));
 }
 
+// v_perm selector tables for the escape-dense lanes (S0 = data word,
+// S1 = 0x7D7D7D7D; selector bytes 0-3 pick S1, 4-7 pick S0, 0x0C gives 0):
+//   expand[p]:  the word's bytes with "7D" inserted before each byte whose
+//               bit is set in the 4-bit pattern p (lo, hi: 8 output bytes)
+//   compact[p]: the bytes whose bit is set in p, in order
+struct SelTables {
+    uint32_t expand[16][2];
+    uint32_t compact[16];
+};
+__device__ __forceinline__ void fill_sel_tables(SelTables *t) {
+    if (threadIdx.x < 16u) {
+        const uint32_t p = threadIdx.x;
+        uint32_t seq[8], m = 0, c[4], mc = 0;
+        for (uint32_t k = 0; k < 4; ++k) {
+            if ((p >> k) & 1u) {
+                seq[m++] = 0u;
+                c[mc++] = 4u + k;
+            }
+            seq[m++] = 4u + k;
+        }
+        while (m < 8) seq[m++] = 0x0Cu;
+        while (mc < 4) c[mc++] = 0x0Cu;
+        t->expand[p][0] = seq[0] | seq[1] << 8 | seq[2] << 16 | seq[3] << 24;
+        t->expand[p][1] = seq[4] | seq[5] << 8 | seq[6] << 16 | seq[7] << 24;
+        t->compact[p] = c[0] | c[1] << 8 | c[2] << 16 | c[3] << 24;
+    }
+    __syncthreads();
+}
+// 4-bit pattern of the bytes flagged 0x80 in m (bit k = byte k)
+__device__ __forceinline__ uint32_t byte_pattern(uint32_t m) {
+    return ((((m >> 7) & 0x01010101u) * 0x01020408u) >> 24) & 0xFu;
+}
+__device__ __forceinline__ void st4u(uint8_t *p, uint32_t v) { __builtin_memcpy(p, &v, 4); }
+// exactly n (0..8) bytes of lo||hi at q: whole dwords where they fit, bytes for the rest
+__device__ __forceinline__ void st_exact8(uint8_t *q, uint32_t lo, uint32_t hi, uint32_t n) {
+    if (n >= 4u) {
+        st4u(q, lo);
+        q += 4;
+        n -= 4u;
+        lo = hi;
+    }
+    if (n == 4u) {
+        st4u(q, lo);
+        return;
+    }
+    for (uint32_t t = 0; t < n; ++t) q[t] = (uint8_t)(lo >> (8 * t));
+}
+
 __global__ __launch_bounds__(256) void k_hdlc_count(const uint8_t *pkt, const uint64_t *off, const uint32_t *len,
                                                     uint64_t *flen, uint32_t n) {
     const uint32_t lane = threadIdx.x & 63u, rl = lane & 15u;
@@ -163,6 +211,8 @@ __global__ __launch_bounds__(256) void k_hdlc_count(const uint8_t *pkt, const ui
 
 __global__ __launch_bounds__(256) void k_hdlc_write(const uint8_t *pkt, const uint64_t *off, const uint32_t *len,
                                                     const uint64_t *foff, uint8_t *out, uint32_t n) {
+    __shared__ SelTables tab;
+    fill_sel_tables(&tab);
     const uint32_t lane = threadIdx.x & 63u, rl = lane & 15u;
     const uint32_t g0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, ng = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t g = g0; 4ull * g < n; g += ng) {
@@ -185,17 +235,22 @@ __global__ __launch_bounds__(256) void k_hdlc_write(const uint8_t *pkt, const ui
             uint8_t *q = o + base + (incl - sz);
             if (esc == 0 && nb == 16) {
                 st16(q, v);
-            } else {
-                // HDLC.escape: ESC first, then FLAG (TCPInterface.py:50-52); per byte the same
+            } else if (nb) {
+                // HDLC.escape (TCPInterface.py:50-52: ESC first, then FLAG; per
+                // byte the same: 7D x^0x20): each word expands through one
+                // selector pair into 4..8 bytes, stored exactly
                 const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
                 uint32_t wpos = 0;
-                for (uint32_t k = 0; k < nb; ++k) {
-                    const uint8_t c = (uint8_t)(wv[k >> 2] >> (8 * (k & 3)));
-                    if (c == ESC || c == FLAG) {
-                        q[wpos++] = ESC;
-                        q[wpos++] = c ^ ESC_MASK;
-                    } else {
-                        q[wpos++] = c;
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    if (4u * j < nb) {
+                        const uint32_t e = escbytes(wv[j]);            // bytes past nb are 0: never escapes
+                        const uint32_t pat = byte_pattern(e);
+                        const uint32_t x = wv[j] ^ (e >> 2);           // 0x80 -> 0x20 in the escaped bytes
+                        const uint32_t cnt = min(4u, nb - 4u * j) + __builtin_popcount(e);
+                        st_exact8(q + wpos, __builtin_amdgcn_perm(x, 0x7D7D7D7Du, tab.expand[pat][0]),
+                                  __builtin_amdgcn_perm(x, 0x7D7D7D7Du, tab.expand[pat][1]), cnt);
+                        wpos += cnt;
                     }
                 }
             }
@@ -278,6 +333,8 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, const
                                                        uint64_t max_pairs, uint32_t hw_mtu, uint32_t ifac_size,
                                                        uint8_t *out, uint64_t *frame_off, uint32_t *frame_len,
                                                        int32_t *status) {
+    __shared__ SelTables tab;
+    fill_sel_tables(&tab);
     const uint64_t nf = *nflags_p;
     uint64_t npairs = nf > 1 ? nf - 1 : 0;
     if (npairs > max_pairs) npairs = max_pairs;
@@ -314,10 +371,19 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, const
             uint8_t *q = o + kept_total + (incl - kept);
             if (ndrop == 0 && nb == 16) {
                 st16(q, u32x4{y[0], y[1], y[2], y[3]});
-            } else {
+            } else if (nb) {
+                // each word's kept bytes through one compaction selector, stored exactly
                 uint32_t t = 0;
-                for (uint32_t j = 0; j < nb; ++j)
-                    if (!((drop[j >> 2] >> (8 * (j & 3) + 7)) & 1u)) q[t++] = (uint8_t)(y[j >> 2] >> (8 * (j & 3)));
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    if (4u * j < nb) {
+                        const uint32_t m = min(4u, nb - 4u * j);
+                        const uint32_t keep = byte_pattern(~drop[j] & 0x80808080u) & ((1u << m) - 1u);
+                        const uint32_t cnt = __builtin_popcount(keep);
+                        st_exact8(q + t, __builtin_amdgcn_perm(y[j], 0u, tab.compact[keep]), 0u, cnt);
+                        t += cnt;
+                    }
+                }
             }
             kept_total += row_sum16(kept);
             carry = row_sum16(rl == 15 ? v.w >> 24 : 0u);      // the window's last byte, to every lane

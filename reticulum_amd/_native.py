@@ -9,7 +9,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librnstok.so")
+# RNSTOK_LIB: an alternative build of the same library (A/B experiments, tools/)
+LIB_PATH = os.environ.get("RNSTOK_LIB") or os.path.join(_HERE, "librnstok.so")
 
 RT_OK, RT_E_INVAL, RT_E_HIP, RT_E_NOMEM, RT_E_NODEV = 0, -1, -2, -3, -4
 RT_F_SORT_BY_LENGTH = 1

@@ -9,6 +9,8 @@ ident: 2^20 x 500 B with a fresh HKDF-derived key per packet (Identity.encrypt
       keying, Identity.py:837-846): times rt_hkdf (32 B shared key, 16 B
       salt -> 64 B), the derived keyset (HKDF + key setup, incl. allocation)
       and encrypt / decrypt with key_idx = packet index
+resource: Resource hashmaps: 1024 resources x 1024 parts
+      x 464 B, map hashes with and without the 224-part collision guard
 wire: the interface path around the token, 2^20 raw
       500-B packets on the device: HDLC framing into one stream, deframing
       that stream (the read loop), IFAC mask and unmask (16-B IFACs, 64-B
@@ -146,6 +148,9 @@ def main():
     elif cfg == "wire":
         print(json.dumps(wire_config(dev, g, args.steps)))
         return
+    elif cfg == "resource":
+        print(json.dumps(resource_config(dev, g, args.steps)))
+        return
     else:
         raise SystemExit("unknown config " + cfg)
 
@@ -172,6 +177,48 @@ def main():
                 "plaintext_gib_per_step": bytes_pt / 2**30,
                 "gib_s": (bytes_pt if cfg == "c5" else 2 * bytes_pt) / ((em + dm) * 1e-3) / 2**30})
     print(json.dumps(res))
+
+
+def resource_config(dev, g, steps):
+    """Resource hashmaps (Resource.py:426-468, 505-506) for 1024 resources of
+    1024 parts x 464 B (SDU) each, one launch: map hash = SHA-256(part ||
+    random_hash)[:4] per part (8 compressions for 464 + 4 B), and the
+    collision guard over the previous 224 parts of the same resource."""
+    import torch
+    from reticulum_amd import device
+    n_res, per, sdu, guard = 1024, 1024, 464, 224
+    n = n_res * per
+    data = torch.randint(0, 256, (n * sdu,), dtype=torch.uint8, device=dev, generator=g)
+    salts = torch.randint(0, 256, (n_res, 4), dtype=torch.uint8, device=dev, generator=g)
+    off = torch.arange(n, dtype=torch.int64, device=dev) * sdu
+    ln = torch.full((n,), sdu, dtype=torch.int32, device=dev)
+    res = torch.arange(n, dtype=torch.int32, device=dev) // per
+    out = torch.empty(n * 4, dtype=torch.uint8, device=dev)
+    first = torch.empty(n_res, dtype=torch.int32, device=dev)
+    times = {}
+    for name, gd in (("map_hashes", 0), ("map_hashes+collision_guard", guard)):
+        for _ in range(2):
+            device.map_hashes(data, out, salts, off, ln, res, sdu=sdu, guard=gd, first_collision=first)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for a, b in ev:
+            a.record()
+            device.map_hashes(data, out, salts, off, ln, res, sdu=sdu, guard=gd, first_collision=first)
+            b.record()
+        torch.cuda.synchronize()
+        ms = sorted(a.elapsed_time(b) for a, b in ev)[steps // 2]
+        times[name] = {"ms": ms, "parts_s": n / (ms * 1e-3), "input_gb_s": n * sdu / (ms * 1e-3) / 1e9}
+    # size-independent check: a part equal to another part of the same resource
+    # hashes equally, so one repeat planted inside the guard window is found
+    # (first_collision holds global part indices); its neighbour stays clean
+    rows = data.view(n, sdu)
+    rows[5 * per + 100] = rows[5 * per + 40]
+    device.map_hashes(data, out, salts, off, ln, res, sdu=sdu, guard=guard, first_collision=first)
+    torch.cuda.synchronize()
+    f = first.cpu()
+    h = out.view(n, 4)
+    ok = int(f[5]) == 5 * per + 100 and int(f[4]) == -1 and torch.equal(h[5 * per + 100], h[5 * per + 40])
+    return {"config": "resource", "resources": n_res, "parts_per_resource": per, "sdu": sdu, "guard": guard,
+            "ok": ok, "stages": times}
 
 
 def wire_config(dev, g, steps):

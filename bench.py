@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
     ap.add_argument("--length", type=int, default=500, help="plaintext bytes per packet")
     ap.add_argument("--keys", type=int, default=1, help="1 = single link key (c2); 65536 = c3")
+    ap.add_argument("--pt-stride", type=int, default=0, help="bytes between plaintext rows in HBM (0: packed)")
+    ap.add_argument("--tok-stride", type=int, default=0, help="bytes between token rows in HBM (0: packed)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 disables)")
     ap.add_argument("--cpu-workers", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--e2e", action="store_true", default=True, help="also time the PCIe-inclusive path")
@@ -138,10 +140,11 @@ def main():
     tl = rt.token_len(L)
     dev = torch.device("cuda", local)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    pt = torch.randint(0, 256, (n, L), dtype=torch.uint8, device=dev, generator=g)
+    ps, ts = max(args.pt_stride, L), max(args.tok_stride, tl)
+    pt = torch.randint(0, 256, (n, ps), dtype=torch.uint8, device=dev, generator=g)[:, :L]
     iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
-    tok = torch.empty((n, tl), dtype=torch.uint8, device=dev)
-    back = torch.empty((n, tl - 48), dtype=torch.uint8, device=dev)
+    tok = torch.empty((n, ts), dtype=torch.uint8, device=dev)[:, :tl]
+    back = torch.empty((n, max(ps, tl - 48)), dtype=torch.uint8, device=dev)[:, :tl - 48]
     out_len = torch.empty(n, dtype=torch.int32, device=dev)
     status = torch.empty(n, dtype=torch.int32, device=dev)
     kg = torch.Generator().manual_seed(7)
@@ -238,6 +241,7 @@ def main():
                                 f"c3: 2^20 x 500 B packets per GPU, {args.keys} per-packet keys")
                    if (n == 1 << 20 and L == 500) else f"{n} x {L} B packets per GPU, {args.keys} key(s)",
                    "packets_per_gpu": n, "plaintext_bytes": L, "token_bytes": tl, "keys": args.keys,
+                   "row_strides": {"plaintext": ps, "token": ts},
                    "step": "encrypt+MAC then verify+decrypt of the same batch", "parallelism": f"shard{world}"},
         "kernels": {
             "encrypt": {"ms": enc_avg, "packets_s": n / (enc_avg * 1e-3),

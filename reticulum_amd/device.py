@@ -21,6 +21,19 @@ def _p(t):
     return t.data_ptr()
 
 
+def _p_rows(t):
+    """A (n, row) byte matrix whose rows may sit at any stride >= row (a row
+    view of a wider buffer, e.g. 128-B-aligned token rows): bytes within a
+    row contiguous; the row stride is passed to the library separately."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("device API needs tensors in device memory")
+    if t.dim() != 2 or (t.shape[1] > 1 and t.stride(1) != 1) or (t.shape[0] > 1 and t.stride(0) < t.shape[1]):
+        raise ValueError("expected an (n, row) matrix with contiguous rows")
+    return t.data_ptr()
+
+
 def _stream(stream):
     s = stream if stream is not None else torch.cuda.current_stream()
     return s.cuda_stream
@@ -33,8 +46,9 @@ def _check_u8(*ts):
 
 
 def encrypt_uniform(ks: KeySet, pt, pt_len, iv, tok, key_idx=None, stream=None):
-    """pt: (n, pt_stride) uint8; iv: (n, 16) uint8; tok: (n, tok_stride) uint8
-    with tok_stride >= token_len(pt_len); key_idx: (n,) int32 or None."""
+    """pt: (n, >= pt_len) uint8 rows; iv: (n, 16) uint8; tok: (n, >=
+    token_len(pt_len)) uint8 rows; key_idx: (n,) int32 or None.  pt and tok
+    may be row views of wider buffers (their row stride is used)."""
     _check_u8(pt, iv, tok)
     n = pt.shape[0]
     if iv.numel() < 16 * n or tok.shape[0] != n:
@@ -42,8 +56,8 @@ def encrypt_uniform(ks: KeySet, pt, pt_len, iv, tok, key_idx=None, stream=None):
     if key_idx is not None and (key_idx.numel() != n or key_idx.dtype != torch.int32):
         raise ValueError("key_idx must be (n,) int32")
     lib = _native.load()
-    _native.check(lib.rt_encrypt_uniform(ks.handle, _p(pt), pt.stride(0), pt_len, _p(key_idx), _p(iv), _p(tok),
-                                         tok.stride(0), n, _stream(stream)))
+    _native.check(lib.rt_encrypt_uniform(ks.handle, _p_rows(pt), pt.stride(0), pt_len, _p(key_idx), _p(iv),
+                                         _p_rows(tok), tok.stride(0), n, _stream(stream)))
 
 
 def decrypt_uniform(ks: KeySet, tok, tok_len, pt, out_len, status, key_idx=None, stream=None):
@@ -54,7 +68,7 @@ def decrypt_uniform(ks: KeySet, tok, tok_len, pt, out_len, status, key_idx=None,
     if pt.shape[0] != n or out_len.numel() != n or status.numel() != n:
         raise ValueError("shape mismatch")
     lib = _native.load()
-    _native.check(lib.rt_decrypt_uniform(ks.handle, _p(tok), tok.stride(0), tok_len, _p(key_idx), _p(pt),
+    _native.check(lib.rt_decrypt_uniform(ks.handle, _p_rows(tok), tok.stride(0), tok_len, _p(key_idx), _p_rows(pt),
                                          pt.stride(0), _p(out_len), _p(status), n, _stream(stream)))
 
 

@@ -440,3 +440,30 @@ def test_long_decrypt_statuses(rt, klen):
         else:
             assert st_long[i] == 0 and ol_long[i] == 16 * m - padn, i
             assert np.array_equal(b_long[i, : 16 * m - padn], x[i, : 16 * m - padn]), i
+
+
+def test_device_uniform_row_views(rt):
+    """The uniform device entry points take row views of wider buffers (row
+    stride >= row): tokens and plaintexts equal the packed-layout launch."""
+    import torch
+    from reticulum_amd import device
+    n, L = 5000, 500
+    tl = rt.token_len(L)
+    g = torch.Generator(device="cuda").manual_seed(21)
+    wide = torch.randint(0, 256, (n, 512), dtype=torch.uint8, device="cuda", generator=g)
+    iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
+    ks = rt.KeySet(bytes(range(64)))
+    tok_a = torch.empty((n, tl), dtype=torch.uint8, device="cuda")
+    device.encrypt_uniform(ks, wide[:, :L].contiguous(), L, iv, tok_a)
+    tok_b = torch.zeros((n, 640), dtype=torch.uint8, device="cuda")
+    device.encrypt_uniform(ks, wide[:, :L], L, iv, tok_b[:, :tl])
+    back = torch.zeros((n, 576), dtype=torch.uint8, device="cuda")
+    ol = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    device.decrypt_uniform(ks, tok_b[:, :tl], tl, back[:, :tl - 48], ol, st)
+    torch.cuda.synchronize()
+    assert torch.equal(tok_a, tok_b[:, :tl])
+    assert int((tok_b[:, tl:] != 0).sum()) == 0             # bytes past each row untouched
+    assert int(st.abs().sum()) == 0 and torch.equal(back[:, :L], wide[:, :L])
+    with pytest.raises(ValueError):
+        device.encrypt_uniform(ks, wide[:, ::2], 256, iv, tok_a)       # bytes of a row not contiguous

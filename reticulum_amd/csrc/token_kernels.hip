@@ -429,7 +429,17 @@ __global__ __launch_bounds__(256) void k_encrypt_long(EncArgs a) {
 // one barrier per quad step.  Single key, uniform lengths.
 constexpr uint32_t L4_TOK = 128, L4_AES_WAVES = 8, L4_THREADS = 64u * (L4_AES_WAVES + 2u);
 constexpr uint32_t L4_RING = LDS_ENC_BYTES;                              // after the table image
-constexpr uint32_t LDS_ENC_LONG4_BYTES = L4_RING + 2u * L4_TOK * 64u;     // + 2 slots x 128 tokens x 64 B
+// The ring holds 2 * L4_PHASE quads: AES waves fill L4_PHASE quads per
+// barrier while the hashing waves consume the previous L4_PHASE.  Two quads
+// per phase (half the barriers, a 160 KiB image) measured the same as one
+// (c4 shard 0.999 vs 0.997 ms): the fused kernel's excess over its AES side
+// alone (0.91 ms; hashing side alone 0.73) is SIMD contention, not barrier
+// jitter.
+#ifndef RNSTOK_L4_PHASE
+#define RNSTOK_L4_PHASE 1
+#endif
+constexpr uint32_t L4_PHASE = RNSTOK_L4_PHASE, L4_SLOTS = 2u * L4_PHASE;
+constexpr uint32_t LDS_ENC_LONG4_BYTES = L4_RING + L4_SLOTS * L4_TOK * 64u;   // + slots x 128 tokens x 64 B
 
 // DPP quad_perm: lane j of each group of four reads lane (j + K) & 3.
 template <int K>
@@ -523,7 +533,11 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
                 uint32_t cq[4];
 #pragma unroll
                 for (int b = 0; b < 4; ++b) {
+#ifndef RNSTOK_L4_PROBE_SHA_ONLY        // timing probe: no AES (wrong tokens)
                     cq[b] = enc_block4<NR>(x[b] ^ prev, rk, LN);
+#else
+                    cq[b] = x[b] ^ prev;
+#endif
                     prev = cq[b];
                 }
                 const uint32_t nst = k < nq ? 4u : tb;
@@ -531,26 +545,32 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
 #pragma unroll
                 for (int b = 0; b < 4; ++b)
                     if (valid && (uint32_t)b < nst) st32u(Ck + 16 * b, cq[b]);
-                lds_w *ring = (lds_w *)(uintptr_t)(L4_RING + ((k & 1u) * L4_TOK + slot) * 64u + 4u * col);
+                lds_w *ring = (lds_w *)(uintptr_t)(L4_RING + ((k % L4_SLOTS) * L4_TOK + slot) * 64u + 4u * col);
 #pragma unroll
                 for (int b = 0; b < 4; ++b) ring[4 * b] = cq[b];
-                __syncthreads();     // quad k visible to the hashing waves; they are done with slot (k-1)&1
+                // end of a phase: its quads become visible to the hashing
+                // waves, which are done with the previous phase's slots
+                if ((k + 1u) % L4_PHASE == 0u || k == nq) __syncthreads();
             }
-            __syncthreads();         // matches the hashing waves' last step
+            __syncthreads();         // matches the hashing waves' last phase
         } else {
             uint32_t h[8], opad[8];
             load_uniform8(h, a.rec + REC_IPAD);
             load_uniform8(opad, a.rec + REC_OPAD);
             u32x4 prev = valid ? ld16(a.iv + 16ull * p) : u32x4{0u, 0u, 0u, 0u};
             const uint64_t bits = (uint64_t)(64u + 16u + 16u * (nfull + 1u)) * 8u;
-            __syncthreads();         // step 0: nothing to hash yet
-            for (uint32_t k = 1; k <= nq + 1u; ++k) {
-                lds_q *r = (lds_q *)(uintptr_t)(L4_RING + (((k - 1u) & 1u) * L4_TOK + slot) * 64u);
+            __syncthreads();         // phase 0: nothing to hash yet
+            const uint32_t phases = (nq + L4_PHASE) / L4_PHASE;       // the AES waves' phases
+            for (uint32_t j = 1; j <= phases; ++j) {
+              for (uint32_t q = (j - 1u) * L4_PHASE; q < j * L4_PHASE && q <= nq; ++q) {
+                lds_q *r = (lds_q *)(uintptr_t)(L4_RING + ((q % L4_SLOTS) * L4_TOK + slot) * 64u);
                 const u32x4 c0 = r[0], c1 = r[1], c2 = r[2], c3 = r[3];
-                if (k - 1u < nq) {
+                if (q < nq) {
+#ifndef RNSTOK_L4_PROBE_AES_ONLY        // timing probe: no HMAC (wrong tags)
                     uint32_t w[16];
                     sha_units(w, prev, c0, c1, c2);
                     sha256_compress(h, w);
+#endif
                     prev = c3;
                 } else if (valid) {
                     // tail quad: units prev, c0..c_{tb-1} (+ final padding), then the outer hash
@@ -569,7 +589,8 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
                     st16(T, u32x4{bswap(tag[0]), bswap(tag[1]), bswap(tag[2]), bswap(tag[3])});
                     st16(T + 16, u32x4{bswap(tag[4]), bswap(tag[5]), bswap(tag[6]), bswap(tag[7])});
                 }
-                __syncthreads();
+              }
+              __syncthreads();
             }
         }
     }

@@ -72,6 +72,7 @@ __device__ __forceinline__ uint32_t td0(const uint8_t *inv, uint32_t x) {
 
 template <bool DEC>
 __device__ void fill_tables(uint32_t *tab, const uint8_t *sbox, const uint8_t *inv) {
+    // ≈5-9 µs per launch on c2 (a build that skips it: encrypt 0.888 -> 0.879 ms)
     // regions 0,1: 32768 dwords; dword d -> region d>>14, row (d>>6)&255, table (d>>5)&1
     for (uint32_t d = threadIdx.x; d < 32768u; d += blockDim.x) {
         uint32_t x = (d >> 6) & 255u, t = ((d >> 14) << 1) | ((d >> 5) & 1u);

@@ -1009,6 +1009,15 @@ static Shape shape_for(uint32_t n, int max_threads, int n_cu) {
     uint64_t t = (per_cu + 63) / 64 * 64;
     if (t < 64) t = 64;
     if (t > (uint64_t)max_threads) t = max_threads;
+    // Two passes per lane at most: split them evenly over whole sets of 4
+    // waves (e.g. 2^18 packets at 768 threads gave a third of the lanes a
+    // second packet and doubled a latency-bound launch; 512 threads x 2 do
+    // not).  Longer batches keep the widest shape and balance by chunks.
+    if (per_cu > (uint64_t)max_threads && per_cu <= 2ull * (uint64_t)max_threads) {
+        const uint64_t half = (per_cu + 1) / 2;
+        t = (half + 255) / 256 * 256;
+        if (t > (uint64_t)max_threads) t = max_threads;
+    }
     uint64_t g = ((uint64_t)n + t - 1) / t;
     if (g > (uint64_t)n_cu) g = n_cu;
     if (g < 1) g = 1;

@@ -25,6 +25,8 @@
  *   rt_packet_pack_headers  Packet.pack header   RNS/Packet.py:167-228
  *   rt_keyset_create_hkdf  per-packet keying     Identity.py:837-846 (hkdf -> Token(derived_key)),
  *                                                Link.py handshake key derivation
+ *   rt_verify_trials*  ratchet trial loop        Identity.py:865-878 (first ratchet whose key
+ *                                                opens the token; Token.py:77-84,114)
  *
  * Conventions
  *  - No exceptions cross the boundary.  API misuse returns a negative RT_E_*
@@ -183,6 +185,26 @@ rt_keyset *rt_keyset_create_hkdf(rt_ctx *ctx, const uint8_t *ikm, uint64_t ikm_s
                                  const uint8_t *salt, uint64_t salt_stride, uint32_t salt_len,
                                  const uint8_t *context, uint32_t context_len, uint32_t key_len, uint32_t n,
                                  void *stream);
+
+/* ---- ratchet trials (Identity.decrypt, RNS/Identity.py:865-878) --------- */
+/* Identity.decrypt tries the receiver's ratchets in order and keeps the first
+ * whose derived token key opens the token.  Token t has the candidate keys
+ * pair_key[pair_off[t] .. pair_off[t+1]) of the key set, in the caller's
+ * ratchet order (pair_off: n_tok + 1 entries from 0 to n_pairs).  first[t]
+ * receives the rank (0-based, within token t's candidates) of the first
+ * candidate whose HMAC-SHA256 tag verifies over a well-formed token
+ * (len >= 64, len - 48 a multiple of 16; Token.py:77-84,114), or 0xFFFFFFFF.
+ * Decrypting each opened token with that key (rt_decrypt* with key_idx)
+ * completes the loop: a BAD_PAD there means no ratchet opens it, as every
+ * later candidate that verifies is the same key.  rt_verify_trials takes
+ * DEVICE pointers and only enqueues; _host takes HOST pointers, validates
+ * the CSR and key indices, and returns when `first` is filled. */
+int rt_verify_trials(const rt_keyset *ks, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,
+                     const uint32_t *pair_off, const uint32_t *pair_key, uint32_t *first, uint32_t n_tok,
+                     uint32_t n_pairs, void *stream);
+int rt_verify_trials_host(const rt_keyset *ks, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,
+                          const uint32_t *pair_off, const uint32_t *pair_key, uint32_t *first, uint32_t n_tok,
+                          uint32_t n_pairs);
 
 /* ---- Resource hashmap (RNS/Resource.py:426-468, 505-506) ---------------- */
 /* map_hash_j = SHA-256(part_j || salt)[:4] for n_parts parts, DEVICE pointers.

@@ -42,6 +42,8 @@ SIGNATURES = [
     ("rt_hkdf", _int, [_vp, _vp, _u64, _u32, _vp, _u64, _u32, _vp, _u32, _vp, _u64, _u32, _u32, _vp]),
     ("rt_hkdf_host", _int, [_vp, _vp, _u64, _u32, _vp, _u64, _u32, _vp, _u32, _vp, _u64, _u32, _u32]),
     ("rt_keyset_create_hkdf", _vp, [_vp, _vp, _u64, _u32, _vp, _u64, _u32, _vp, _u32, _u32, _u32, _vp]),
+    ("rt_verify_trials", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp]),
+    ("rt_verify_trials_host", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32]),
     ("rt_map_hashes", _int, [_vp, _vp, _vp, _vp, _u64, _u32, _vp, _u32, _vp, _u32, _u32, _vp, _vp, _u32, _vp]),
     ("rt_resource_hashmap_host", _int, [_vp, _vp, _u64, _u32, _vp, _u32, _u32, _vp, _vp]),
     ("rt_hdlc_frame_workspace_bytes", _u64, [_u32]),

@@ -385,6 +385,65 @@ static int ensure_work(rt_ctx *c, uint64_t bytes) {
 
 static uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
 
+// ----------------------------------------------------------- ratchet trials
+
+int rt_verify_trials(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,
+                     const uint32_t *pair_off, const uint32_t *pair_key, uint32_t *first, uint32_t n_tok,
+                     uint32_t n_pairs, void *stream) {
+    int rc = check_keyset(k);
+    if (rc) return rc;
+    if (n_tok == 0) return RT_OK;
+    if (!tok_off || !tok_len || !pair_off || !first || (n_pairs && (!tok || !pair_key)))
+        return fail(RT_E_INVAL, "rt_verify_trials: null argument");
+    TrialArgs a{};
+    a.rec = k->d_rec; a.tok = tok; a.tok_off = tok_off; a.tok_len = tok_len; a.pair_off = pair_off;
+    a.pair_key = pair_key; a.first = first; a.n_tok = n_tok; a.n_pairs = n_pairs;
+    RT_HIP(hipSetDevice(k->ctx->device), "hipSetDevice");
+    RT_HIP(launch_verify_trials(a, pick(k->ctx, stream)), "verify trials launch");
+    return RT_OK;
+}
+
+int rt_verify_trials_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,
+                          const uint32_t *pair_off, const uint32_t *pair_key, uint32_t *first, uint32_t n_tok,
+                          uint32_t n_pairs) {
+    int rc = check_keyset(k);
+    if (rc) return rc;
+    if (n_tok == 0) return RT_OK;
+    if (!tok_off || !tok_len || !pair_off || !first || (n_pairs && !pair_key))
+        return fail(RT_E_INVAL, "rt_verify_trials_host: null argument");
+    if (pair_off[0] != 0 || pair_off[n_tok] != n_pairs)
+        return fail(RT_E_INVAL, "rt_verify_trials_host: pair_off must run from 0 to n_pairs");
+    uint64_t tok_ext = 0;
+    for (uint32_t t = 0; t < n_tok; ++t) {
+        if (pair_off[t + 1] < pair_off[t]) return fail(RT_E_INVAL, "rt_verify_trials_host: pair_off not ascending");
+        tok_ext = std::max<uint64_t>(tok_ext, tok_off[t] + tok_len[t]);
+    }
+    for (uint32_t j = 0; j < n_pairs; ++j)
+        if (pair_key[j] >= k->n_keys) return fail(RT_E_INVAL, "pair_key out of range");
+    if (tok_ext && !tok) return fail(RT_E_INVAL, "rt_verify_trials_host: null tokens");
+    rt_ctx *c = k->ctx;
+    std::lock_guard<std::mutex> g(c->mu);
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    const uint64_t o_tok = 0, o_to = align16(o_tok + std::max<uint64_t>(tok_ext, 1)), o_tl = align16(o_to + 8ull * n_tok),
+                   o_po = align16(o_tl + 4ull * n_tok), o_pk = align16(o_po + 4ull * (n_tok + 1)),
+                   o_fi = align16(o_pk + 4ull * std::max<uint32_t>(n_pairs, 1)), total = align16(o_fi + 4ull * n_tok);
+    if ((rc = ensure_work(c, total))) return rc;
+    uint8_t *w = c->d_work;
+    hipStream_t s = c->stream;
+    if (tok_ext) RT_HIP(hipMemcpyAsync(w + o_tok, tok, tok_ext, hipMemcpyHostToDevice, s), "H2D tok");
+    RT_HIP(hipMemcpyAsync(w + o_to, tok_off, 8ull * n_tok, hipMemcpyHostToDevice, s), "H2D tok_off");
+    RT_HIP(hipMemcpyAsync(w + o_tl, tok_len, 4ull * n_tok, hipMemcpyHostToDevice, s), "H2D tok_len");
+    RT_HIP(hipMemcpyAsync(w + o_po, pair_off, 4ull * (n_tok + 1), hipMemcpyHostToDevice, s), "H2D pair_off");
+    if (n_pairs) RT_HIP(hipMemcpyAsync(w + o_pk, pair_key, 4ull * n_pairs, hipMemcpyHostToDevice, s), "H2D pair_key");
+    if ((rc = rt_verify_trials(k, w + o_tok, (const uint64_t *)(w + o_to), (const uint32_t *)(w + o_tl),
+                               (const uint32_t *)(w + o_po), (const uint32_t *)(w + o_pk), (uint32_t *)(w + o_fi),
+                               n_tok, n_pairs, s)))
+        return rc;
+    RT_HIP(hipMemcpyAsync(first, w + o_fi, 4ull * n_tok, hipMemcpyDeviceToHost, s), "D2H first");
+    RT_HIP(hipStreamSynchronize(s), "stream sync");
+    return RT_OK;
+}
+
 int rt_encrypt_host(const rt_keyset *k, const uint8_t *pt, const uint64_t *pt_off, const uint32_t *pt_len,
                     const uint32_t *key_idx, const uint8_t *iv, uint8_t *tok, const uint64_t *tok_off, uint32_t n) {
     int rc = check_keyset(k);

@@ -826,6 +826,61 @@ __global__ __launch_bounds__(1024) void k_decrypt_long(DecArgs a) {
     }
 }
 
+// --------------------------------------------------------- ratchet trials --
+//
+// Identity.decrypt (RNS/Identity.py:865-878) tries the receiver's ratchets in
+// order and keeps the first whose derived token key opens the token (a wrong
+// key raises in Token.decrypt and the loop moves on).  One lane per (token,
+// candidate key) pair: HMAC-SHA256 over iv||ct under the candidate's
+// midstates (Token.py:77-84), compared with the tag; the smallest matching
+// rank per token wins (atomicMin).  A token that is not well-formed (len < 64
+// or a ciphertext that is not whole blocks) never opens (Token.py:114), so it
+// never matches.  The caller then decrypts each opened token with its key.
+__global__ __launch_bounds__(256) void k_verify_trials(TrialArgs a) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= a.n_pairs) return;
+    uint32_t lo = 0, hi = a.n_tok;             // token of pair j: last t with pair_off[t] <= j
+    while (hi - lo > 1u) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.pair_off[mid] <= j)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    const uint32_t t = lo, T = a.tok_len[t];
+    if (T < 64u || ((T - 48u) & 15u)) return;
+    const uint8_t *Kt = a.tok + a.tok_off[t];
+    const uint32_t *r = a.rec + (uint64_t)a.pair_key[j] * REC_WORDS;
+    uint32_t h[8], opad[8], tag[8];
+    load8(h, r + REC_IPAD);
+    const uint32_t M = T - 32u, full = M >> 6;
+    for (uint32_t i = 0; i < full; ++i) {
+        const uint8_t *B = Kt + 64ull * i;
+        uint32_t w[16];
+        sha_units(w, ld16(B), ld16(B + 16), ld16(B + 32), ld16(B + 48));
+        sha256_compress(h, w);
+    }
+    const uint32_t fu = (M - 64u * full) >> 4;
+    const uint8_t *R = Kt + 64ull * full;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    sha_final_units(h, fu, fu > 0 ? ld16(R) : z, fu > 1 ? ld16(R + 16) : z, fu > 2 ? ld16(R + 32) : z,
+                    (uint64_t)(64u + M) * 8u);
+    load8(opad, r + REC_OPAD);
+    hmac_outer(tag, h, opad);
+    const u32x4 r0 = ld16(Kt + M), r1 = ld16(Kt + M + 16);
+    const uint32_t diff = (r0.x ^ bswap(tag[0])) | (r0.y ^ bswap(tag[1])) | (r0.z ^ bswap(tag[2])) |
+                          (r0.w ^ bswap(tag[3])) | (r1.x ^ bswap(tag[4])) | (r1.y ^ bswap(tag[5])) |
+                          (r1.z ^ bswap(tag[6])) | (r1.w ^ bswap(tag[7]));
+    if (diff == 0u) atomicMin(a.first + t, j - a.pair_off[t]);
+}
+
+hipError_t launch_verify_trials(const TrialArgs &a, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(a.first, 0xFF, 4ull * a.n_tok, s);
+    if (e != hipSuccess || a.n_pairs == 0) return e;
+    hipLaunchKernelGGL(k_verify_trials, dim3((a.n_pairs + 255u) / 256u), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------ length bucketing --
 //
 // Three small passes (histogram, scan, scatter) build a permutation that

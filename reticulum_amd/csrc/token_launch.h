@@ -42,6 +42,21 @@ struct DecArgs {
     uint32_t n;
 };
 
+// Ratchet trials (Identity.py:865-878): pairs j in [pair_off[t],
+// pair_off[t+1]) try key pair_key[j] on token t; first[t] = the rank of the
+// first pair whose HMAC verifies over a well-formed token, or 0xFFFFFFFF.
+struct TrialArgs {
+    const uint32_t *rec;
+    const uint8_t *tok;
+    const uint64_t *tok_off;
+    const uint32_t *tok_len;
+    const uint32_t *pair_off;   // n_tok + 1 entries, pair_off[0] = 0, pair_off[n_tok] = n_pairs
+    const uint32_t *pair_key;
+    uint32_t *first;
+    uint32_t n_tok, n_pairs;
+};
+hipError_t launch_verify_trials(const TrialArgs &a, hipStream_t s);
+
 // HKDF-SHA256 over n items (hkdf_kernels.hip): item i reads ikm + i*ikm_stride
 // and salt + i*salt_stride (salt null or salt_len 0: zero key), shares the
 // context, writes `length` bytes at out + i*out_stride.

@@ -72,6 +72,21 @@ def decrypt_uniform(ks: KeySet, tok, tok_len, pt, out_len, status, key_idx=None,
                                          pt.stride(0), _p(out_len), _p(status), n, _stream(stream)))
 
 
+def verify_trials(ks: KeySet, tok, tok_off, tok_len, pair_off, pair_key, first, stream=None):
+    """Ratchet trials (Identity.py:865-878) over device buffers: token t is
+    tok[tok_off[t] : +tok_len[t]] (int64 / int32), its candidates are
+    pair_key[pair_off[t] : pair_off[t+1]] (int32, pair_off (n+1,) int32 from
+    0); first (n,) int32 receives the rank of the first candidate whose key
+    opens token t, or -1."""
+    _check_u8(tok)
+    n = tok_off.numel()
+    if tok_len.numel() != n or pair_off.numel() != n + 1 or first.numel() != n:
+        raise ValueError("shape mismatch")
+    lib = _native.load()
+    _native.check(lib.rt_verify_trials(ks.handle, _p(tok), _p(tok_off), _p(tok_len), _p(pair_off), _p(pair_key),
+                                       _p(first), n, pair_key.numel(), _stream(stream)))
+
+
 def _workspace(n, device):
     lib = _native.load()
     return torch.empty(int(lib.rt_workspace_bytes(n)), dtype=torch.uint8, device=device)

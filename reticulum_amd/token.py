@@ -162,6 +162,53 @@ class KeySet:
         out, status, _ = self._decrypt_raw(tokens, key_idx)
         return out, status
 
+    def verify_trials(self, tokens, candidates):
+        """Identity.decrypt's ratchet loop (Identity.py:865-878) over a batch:
+        ``candidates[t]`` lists key indices of this key set to try on token t,
+        in ratchet order.  Returns an int64 array: the first candidate key
+        index whose HMAC verifies over well-formed token t, or -1."""
+        toks = tokens if isinstance(tokens, Packed) else Packed.from_list(list(tokens))
+        n = len(toks)
+        if len(candidates) != n:
+            raise ValueError("need one candidate list per token")
+        counts = np.fromiter((len(c) for c in candidates), dtype=np.uint32, count=n)
+        pair_off = np.zeros(n + 1, dtype=np.uint32)
+        np.cumsum(counts, out=pair_off[1:])
+        pair_key = np.fromiter((k for c in candidates for k in c), dtype=np.int64, count=int(pair_off[-1]))
+        if pair_key.size and (pair_key.min() < 0 or pair_key.max() >= self.n_keys):
+            raise ValueError("candidate key index out of range")
+        pair_key = pair_key.astype(np.uint32)
+        first = np.zeros(n, dtype=np.uint32)
+        if n:
+            _native.check(self._lib.rt_verify_trials_host(self._ptr, _ptr(toks.buf), _ptr(toks.off),
+                                                          _ptr(toks.length), _ptr(pair_off), _ptr(pair_key),
+                                                          _ptr(first), n, int(pair_off[-1])))
+        out = np.full(n, -1, dtype=np.int64)
+        hit = first != 0xFFFFFFFF
+        out[hit] = pair_key[pair_off[:-1][hit].astype(np.int64) + first[hit]]
+        return out
+
+    def decrypt_trials(self, tokens, candidates):
+        """verify_trials, then each opened token decrypted with its key.
+        Returns ``(plaintexts: Packed, status, key_used)``: key_used is -1 and
+        status RT_ST_BAD_HMAC where no candidate opens the token (the
+        reference's loop ends with plaintext None, Identity.py:880-886)."""
+        toks = tokens if isinstance(tokens, Packed) else Packed.from_list(list(tokens))
+        key_used = self.verify_trials(toks, candidates)
+        n = len(toks)
+        opened = np.nonzero(key_used >= 0)[0]
+        status = np.full(n, RT_ST_BAD_HMAC, dtype=np.int32)
+        lengths = np.zeros(n, dtype=np.uint32)
+        bufs = [b""] * n
+        if opened.size:
+            sub = Packed.from_list([toks[int(i)] for i in opened])
+            pts, st, _ = self._decrypt_raw(sub, key_idx=key_used[opened])
+            status[opened] = st
+            for j, i in enumerate(opened):
+                bufs[int(i)] = pts[j]
+        out = Packed.from_list(bufs)
+        return out, status, np.where(status == RT_ST_OK, key_used, -1)
+
     def _decrypt_raw(self, tokens, key_idx=None):
         toks = tokens if isinstance(tokens, Packed) else Packed.from_list(list(tokens))
         n = len(toks)

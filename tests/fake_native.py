@@ -90,6 +90,24 @@ class FakeLib:
                 pbuf[region] = 0
         return 0
 
+    def rt_verify_trials_host(self, ks, tok, tok_off, tok_len, pair_off, pair_key, first, n_tok, n_pairs):
+        """first[t] = rank of the first candidate key that opens token t
+        (oracle status OK or BAD_PAD: tag verified over a well-formed token)."""
+        self.calls.append(("rt_verify_trials_host", n_tok, n_pairs))
+        keys = self._keysets[ks]
+        to, tl = _arr(tok_off, np.uint64, n_tok), _arr(tok_len, np.uint32, n_tok)
+        po, pk = _arr(pair_off, np.uint32, n_tok + 1), _arr(pair_key, np.uint32, n_pairs)
+        tbuf = _arr(tok, np.uint8, int(max((to + tl).max(), 1)))
+        out = _arr(first, np.uint32, n_tok)
+        for t in range(n_tok):
+            out[t] = 0xFFFFFFFF
+            token = tbuf[to[t]:to[t] + tl[t]].tobytes()
+            for r, j in enumerate(range(int(po[t]), int(po[t + 1]))):
+                if ctoken.decrypt(keys[pk[j]].tobytes(), token)[0] in (0, 4):
+                    out[t] = r
+                    break
+        return 0
+
     def rt_resource_hashmap_host(self, ctx, data, size, sdu, rh, rh_len, guard, hashmap, first_collision):
         self.calls.append(("rt_resource_hashmap_host", size, sdu, guard))
         stream = _arr(data, np.uint8, size).tobytes()

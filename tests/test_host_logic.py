@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import reticulum_amd as rt
-from tests_helpers import b
+from tests_helpers import b, trial_case
 
 
 @pytest.fixture
@@ -110,3 +110,21 @@ def test_fresh_iv_per_token(fake):
     t = rt.Token(bytes(64))
     a, c = t.encrypt(b"same"), t.encrypt(b"same")
     assert a[:16] != c[:16] and t.decrypt(a) == t.decrypt(c) == b"same"
+
+
+def test_verify_trials_host_layer(fake):
+    """KeySet.verify_trials / decrypt_trials: the CSR the library receives and
+    the first-opening key it returns, per the reference's ratchet loop
+    (Identity.py:865-878); a token under none of its candidates stays closed."""
+    keys, toks, cands, expect = trial_case(5)
+    ks = rt.KeySet(keys)
+    got = ks.verify_trials(toks, cands)
+    assert got.tolist() == expect.tolist()
+    pts, st, used = ks.decrypt_trials(toks, cands)
+    assert used.tolist() == [e if s == rt.RT_ST_OK else -1 for e, s in zip(expect.tolist(), st.tolist())]
+    assert all(st[i] == rt.RT_ST_BAD_HMAC for i in range(len(toks)) if expect[i] < 0)
+    assert ks.verify_trials([], []).size == 0
+    with pytest.raises(ValueError):
+        ks.verify_trials(toks[:2], cands[:1])
+    with pytest.raises(ValueError):
+        ks.verify_trials(toks[:1], [[len(keys)]])

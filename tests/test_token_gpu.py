@@ -467,3 +467,55 @@ def test_device_uniform_row_views(rt):
     assert int(st.abs().sum()) == 0 and torch.equal(back[:, :L], wide[:, :L])
     with pytest.raises(ValueError):
         device.encrypt_uniform(ks, wide[:, ::2], 256, iv, tok_a)       # bytes of a row not contiguous
+
+
+def test_verify_trials_vs_oracle(rt):
+    """Ratchet trials (Identity.py:865-878) on the GPU: the first candidate
+    key that opens each token (right key at a random rank, missing, twice;
+    malformed and short tokens never open), host entry point and
+    decrypt_trials, against the oracle's per-key decrypt."""
+    from tests_helpers import trial_case
+    keys, toks, cands, expect = trial_case(7, n_tok=300, n_keys=33)
+    ks = rt.KeySet(keys)
+    assert ks.verify_trials(toks, cands).tolist() == expect.tolist()
+    pts, st, used = ks.decrypt_trials(toks, cands)
+    from oracle import ctoken
+    for i, tok in enumerate(toks):
+        if expect[i] >= 0:
+            s, p = ctoken.decrypt(keys[expect[i]].tobytes(), tok)
+            assert int(st[i]) == s and (s != 0 or pts[i] == p), i
+        else:
+            assert int(st[i]) == rt.RT_ST_BAD_HMAC and int(used[i]) == -1
+
+
+def test_verify_trials_device_batch(rt):
+    """Device entry point at batch scale: 4096 tokens of 500 B, 16 candidate
+    keys each out of 1024, the right one at a random rank (none for every
+    7th token); bit-exact first ranks."""
+    import torch
+    from reticulum_amd import device
+    rng = np.random.Generator(np.random.PCG64(77))
+    n, L, nk, per = 4096, 500, 1024, 16
+    keys = rng.integers(0, 256, (nk, 64), dtype=np.uint8)
+    ks = rt.KeySet(keys)
+    kidx = rng.integers(0, nk, n).astype(np.int32)
+    pt = torch.from_numpy(rng.integers(0, 256, (n, L), dtype=np.uint8)).cuda()
+    iv = torch.from_numpy(rng.integers(0, 256, (n, 16), dtype=np.uint8)).cuda()
+    tl = rt.token_len(L)
+    tok = torch.empty((n, tl), dtype=torch.uint8, device="cuda")
+    device.encrypt_uniform(ks, pt, L, iv, tok, key_idx=torch.from_numpy(kidx).cuda())
+    cand = rng.integers(0, nk, (n, per)).astype(np.int32)
+    rank = rng.integers(0, per, n)
+    expect = np.full(n, -1, np.int64)
+    for t in range(n):
+        cand[t][cand[t] == kidx[t]] = (kidx[t] + 1) % nk           # no accidental earlier hit
+        if t % 7:
+            cand[t, rank[t]] = kidx[t]
+            expect[t] = rank[t]
+    pair_off = torch.arange(0, n * per + 1, per, dtype=torch.int32, device="cuda")
+    first = torch.empty(n, dtype=torch.int32, device="cuda")
+    device.verify_trials(ks, tok.reshape(-1), torch.arange(n, dtype=torch.int64, device="cuda") * tl,
+                         torch.full((n,), tl, dtype=torch.int32, device="cuda"), pair_off,
+                         torch.from_numpy(cand.reshape(-1)).cuda(), first)
+    torch.cuda.synchronize()
+    assert first.cpu().numpy().astype(np.int64).tolist() == expect.tolist()

@@ -9,6 +9,8 @@ ident: 2^20 x 500 B with a fresh HKDF-derived key per packet (Identity.encrypt
       keying, Identity.py:837-846): times rt_hkdf (32 B shared key, 16 B
       salt -> 64 B), the derived keyset (HKDF + key setup, incl. allocation)
       and encrypt / decrypt with key_idx = packet index
+ratchet: Identity.decrypt's ratchet trial loop: 2^16 x 500 B tokens x 16
+      candidate keys (first opening key per token), then the decrypt
 resource: Resource hashmaps: 1024 resources x 1024 parts
       x 464 B, map hashes with and without the 224-part collision guard
 wire: the interface path around the token, 2^20 raw
@@ -151,6 +153,9 @@ def main():
     elif cfg == "resource":
         print(json.dumps(resource_config(dev, g, args.steps)))
         return
+    elif cfg == "ratchet":
+        print(json.dumps(ratchet_config(dev, g, args.steps)))
+        return
     else:
         raise SystemExit("unknown config " + cfg)
 
@@ -177,6 +182,64 @@ def main():
                 "plaintext_gib_per_step": bytes_pt / 2**30,
                 "gib_s": (bytes_pt if cfg == "c5" else 2 * bytes_pt) / ((em + dm) * 1e-3) / 2**30})
     print(json.dumps(res))
+
+
+def ratchet_config(dev, g, steps):
+    """Identity.decrypt's ratchet loop (Identity.py:865-878) at batch scale:
+    2^16 tokens of 500 B, each tried against 16 candidate keys (out of 65 536
+    derived keys) with the opening key at a uniform random rank: the trial
+    pass (1 M HMAC verifications) and the decrypt of the opened tokens with
+    their keys."""
+    import torch
+    import reticulum_amd as rt
+    from reticulum_amd import device
+    n, L, nk, per = 1 << 16, 500, 65536, 16
+    tl = rt.token_len(L)
+    ks = rt.KeySet(torch.randint(0, 256, (nk, 64), dtype=torch.uint8).numpy())
+    kidx = torch.randint(0, nk, (n,), dtype=torch.int32, device=dev, generator=g)
+    pt = torch.randint(0, 256, (n, L), dtype=torch.uint8, device=dev, generator=g)
+    iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
+    tok = torch.empty((n, tl), dtype=torch.uint8, device=dev)
+    device.encrypt_uniform(ks, pt, L, iv, tok, key_idx=kidx)
+    cand = torch.randint(0, nk, (n, per), dtype=torch.int32, device=dev, generator=g)
+    rank = torch.randint(0, per, (n,), dtype=torch.int64, device=dev, generator=g)
+    cand[torch.arange(n, device=dev), rank] = kidx
+    pair_off = torch.arange(0, n * per + 1, per, dtype=torch.int32, device=dev)
+    tok_off = torch.arange(n, dtype=torch.int64, device=dev) * tl
+    tok_len = torch.full((n,), tl, dtype=torch.int32, device=dev)
+    first = torch.empty(n, dtype=torch.int32, device=dev)
+    flat, pairs = tok.reshape(-1), cand.reshape(-1)
+    back = torch.empty((n, tl - 48), dtype=torch.uint8, device=dev)
+    ol = torch.empty(n, dtype=torch.int32, device=dev)
+    st = torch.empty(n, dtype=torch.int32, device=dev)
+
+    def trial():
+        device.verify_trials(ks, flat, tok_off, tok_len, pair_off, pairs, first)
+
+    def opened():
+        key = cand.gather(1, first.clamp(min=0).long().unsqueeze(1)).squeeze(1).contiguous()
+        device.decrypt_uniform(ks, tok, tl, back, ol, st, key_idx=key)
+
+    times = {}
+    for name, fn in (("verify_trials", trial), ("decrypt_opened", opened)):
+        for _ in range(2):
+            fn()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for a, b in ev:
+            a.record()
+            fn()
+            b.record()
+        torch.cuda.synchronize()
+        ms = sorted(a.elapsed_time(b) for a, b in ev)[steps // 2]
+        times[name] = {"ms": ms}
+    times["verify_trials"]["trials_s"] = n * per / (times["verify_trials"]["ms"] * 1e-3)
+    times["decrypt_opened"]["packets_s"] = n / (times["decrypt_opened"]["ms"] * 1e-3)
+    # the opening rank is the first occurrence of the token's key among its
+    # candidates (a random candidate can repeat it earlier)
+    expect = (cand == kidx.unsqueeze(1)).int().argmax(dim=1)
+    ok = torch.equal(first.long(), expect.long()) and bool((st == 0).all()) and torch.equal(back[:, :L], pt)
+    return {"config": "ratchet", "tokens": n, "candidates_per_token": per, "keys": nk, "payload": L, "ok": ok,
+            "stages": times}
 
 
 def resource_config(dev, g, steps):

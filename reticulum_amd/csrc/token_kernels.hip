@@ -599,8 +599,12 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
 
 // --------------------------------------------------------------- decrypt --
 
-template <int NR, bool PERKEY>
-__global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_DEC : WG_DEC) void k_decrypt(DecArgs a) {
+// WG: the workgroup size the kernel is compiled for (its VGPR budget).  One
+// key: 768 threads (168 VGPRs) for batches of several passes, 1024 (128
+// VGPRs, 4 waves/SIMD) when one pass covers the batch (e.g. 16 KiB Resource
+// tokens, one per lane: 512 x 2 passes at 768 was 9 % slower).
+template <int NR, bool PERKEY, int WG = PERKEY ? WG_PERKEY_DEC : WG_DEC>
+__global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
     fill_tables<true>(tab_u32, a.sbox, a.sbox + 256);
 #ifdef RNSTOK_SETPRIO
@@ -1091,6 +1095,8 @@ template <int NR>
 static hipError_t launch_dec_nr(const DecArgs &a, Shape sh, hipStream_t s) {
     if (a.key_idx)
         hipLaunchKernelGGL((k_decrypt<NR, true>), dim3(sh.grid), dim3(sh.threads), LDS_DEC_BYTES, s, a);
+    else if (sh.threads > WG_DEC)
+        hipLaunchKernelGGL((k_decrypt<NR, false, 1024>), dim3(sh.grid), dim3(sh.threads), LDS_DEC_BYTES, s, a);
     else
         hipLaunchKernelGGL((k_decrypt<NR, false>), dim3(sh.grid), dim3(sh.threads), LDS_DEC_BYTES, s, a);
     return hipGetLastError();
@@ -1165,7 +1171,10 @@ hipError_t launch_decrypt(const DecArgs &args, int nr, int n_cu, uint32_t *spare
     if (!a.key_idx && a.tok_len == nullptr && a.uni_len >= 48u + 1024u && ((a.uni_len - 48u) & 15u) == 0 &&
         (uint64_t)a.n <= 128ull * (uint64_t)n_cu)
         return nr == 14 ? launch_dec_long_nr<14>(a, n_cu, s) : launch_dec_long_nr<10>(a, n_cu, s);
-    const Shape sh = shape_for(a.n, a.key_idx ? WG_PERKEY_DEC : WG_DEC, n_cu);
+    // one key and one pass at up to 1024 threads: the 1024-thread instance
+    const uint64_t per_cu = ((uint64_t)a.n + n_cu - 1) / n_cu;
+    const int max_t = a.key_idx ? WG_PERKEY_DEC : (per_cu <= 1024u ? 1024 : WG_DEC);
+    const Shape sh = shape_for(a.n, max_t, n_cu);
     const hipError_t e = balance(a, sh, spare, s);
     if (e != hipSuccess) return e;
     return nr == 14 ? launch_dec_nr<14>(a, sh, s) : launch_dec_nr<10>(a, sh, s);
@@ -1197,8 +1206,10 @@ hipError_t configure_kernels() {
     RT_CFG((k_encrypt_long<10, false>), LDS_ENC_LONG_BYTES);
     RT_CFG((k_encrypt_long<10, true>), LDS_ENC_LONG_BYTES);
     RT_CFG((k_decrypt<14, false>), LDS_DEC_BYTES);
+    RT_CFG((k_decrypt<14, false, 1024>), LDS_DEC_BYTES);
     RT_CFG((k_decrypt<14, true>), LDS_DEC_BYTES);
     RT_CFG((k_decrypt<10, false>), LDS_DEC_BYTES);
+    RT_CFG((k_decrypt<10, false, 1024>), LDS_DEC_BYTES);
     RT_CFG((k_decrypt<10, true>), LDS_DEC_BYTES);
 #undef RT_CFG
     return e;

@@ -142,6 +142,8 @@ __device__ __forceinline__ void load8(uint32_t d[8], const uint32_t *p) {
 // that finish last are the shortest, so the CUs end together.  A static
 // stride over the sorted order gave the first workgroup the longest packet of
 // every pass (c5: 40 % more work than the average CU).
+// The chunk counter (32 bits) may run up to n + 64 x the grid's waves.
+constexpr uint32_t QUEUE_MAX_N = 0xF0000000u;
 __device__ __forceinline__ uint32_t take_chunk(uint32_t *q) {
     uint32_t v = 0u;
     if ((threadIdx.x & 63u) == 0u) v = __hip_atomic_fetch_add(q, 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -149,12 +151,15 @@ __device__ __forceinline__ uint32_t take_chunk(uint32_t *q) {
 }
 // Lane 0 carries the wave's smallest index, so it stays active until the
 // whole wave leaves (lanes past n break out of the last chunk only).
-#define RT_PACKET_LOOP(A, I)                                                                              \
-    for (uint32_t rt_base_ = (A).queue ? take_chunk((A).queue) : blockIdx.x * blockDim.x + (threadIdx.x & ~63u), \
-                  I = rt_base_ + (threadIdx.x & 63u);                                                      \
-         rt_base_ < (A).n && I < (A).n;                                                                    \
-         rt_base_ = (A).queue ? take_chunk((A).queue) : rt_base_ + gridDim.x * blockDim.x,               \
-                  I = rt_base_ + (threadIdx.x & 63u))
+// The index runs in 64 bits so that a batch near 2^32 packets cannot wrap
+// it (the launchers use the chunk counter only below QUEUE_MAX_N).
+#define RT_PACKET_LOOP(A, I)                                                                                 \
+    for (uint64_t rt_base_ = (A).queue ? take_chunk((A).queue) : blockIdx.x * blockDim.x + (threadIdx.x & ~63u), \
+                  rt_i_ = rt_base_ + (threadIdx.x & 63u);                                                     \
+         rt_i_ < (A).n;                                                                                       \
+         rt_base_ = (A).queue ? take_chunk((A).queue) : rt_base_ + (uint64_t)gridDim.x * blockDim.x,         \
+                  rt_i_ = rt_base_ + (threadIdx.x & 63u))                                                     \
+        if (const uint32_t I = (uint32_t)rt_i_; true)
 
 // PKCS7 pad block (PKCS7.py:35-39): r (< 16) payload bytes at p, then 16-r copies of 16-r.
 __device__ __forceinline__ u32x4 pad_block(const uint8_t *p, uint32_t r) {
@@ -957,7 +962,7 @@ hipError_t launch_length_order(const uint32_t *len, uint32_t n, int dec, void *w
     uint32_t *hist = (uint32_t *)((uint8_t *)workspace + ((uint64_t)n * 4 + 255) / 256 * 256);
     // hist[0..SORT_BUCKETS) and the chunk counter right after it, zeroed together
     hipError_t e = hipMemsetAsync(hist, 0, SORT_BUCKETS * 4 + 4, s);
-    *queue = hist + SORT_BUCKETS;
+    *queue = n <= QUEUE_MAX_N ? hist + SORT_BUCKETS : nullptr;   // past it: a static stride over the order
     if (e != hipSuccess) return e;
     const int gh = n_cu < (int)((n + 1023) / 1024) ? n_cu : (int)((n + 1023) / 1024);
     hipLaunchKernelGGL(k_sort_hist, dim3(gh > 0 ? gh : 1), dim3(1024), 0, s, len, n, dec, hist);
@@ -1135,7 +1140,7 @@ static hipError_t launch_enc_long4_nr(const EncArgs &a, int n_cu, hipStream_t s)
 template <class Args>
 static hipError_t balance(Args &a, Shape sh, uint32_t *spare, hipStream_t s) {
     const uint64_t lanes = (uint64_t)sh.grid * (uint64_t)sh.threads;
-    if (a.queue || !spare || a.n <= lanes || a.n % lanes == 0) return hipSuccess;
+    if (a.queue || !spare || a.n <= lanes || a.n % lanes == 0 || a.n > QUEUE_MAX_N) return hipSuccess;
     a.queue = spare;
     return hipMemsetAsync(spare, 0, 4, s);
 }

@@ -317,15 +317,17 @@ def test_sorted_variable_batch_matches_unsorted_and_oracle(rt):
 
 @pytest.mark.parametrize("n", [2, 63, 64, 65, 200])
 @pytest.mark.parametrize("n_keys", [1, 7])
-def test_sorted_small_batches_chunk_edges(rt, n, n_keys):
+@pytest.mark.parametrize("klen", [64, 32])
+def test_sorted_small_batches_chunk_edges(rt, n, n_keys, klen):
     """Length-ordered launches around the 64-packet chunk size of the dynamic
-    packet loop (one partial chunk, exactly one, one plus one packet): the
-    tokens equal the oracle's and sorted decrypt restores every plaintext."""
+    packet loop (one partial chunk, exactly one, one plus one packet), AES-256
+    and AES-128 tokens: the tokens equal the oracle's and sorted decrypt
+    restores every plaintext."""
     import torch
     from reticulum_amd import device
-    rng = np.random.Generator(np.random.PCG64(1000 + n + n_keys))
+    rng = np.random.Generator(np.random.PCG64(1000 + n + n_keys + klen))
     lens = rng.integers(0, 1200, n).astype(np.int32)
-    keys, buf, off, ulens, ivs, kidx = _random_batch(rng, n, lens, n_keys)
+    keys, buf, off, ulens, ivs, kidx = _random_batch(rng, n, lens, n_keys, klen)
     ks = rt.KeySet(keys if n_keys > 1 else keys[0].tobytes())
     ref, toff, tl = _oracle_tokens(keys, buf, off, ulens, ivs, kidx)
     cu = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731

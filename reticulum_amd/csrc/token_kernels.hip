@@ -777,7 +777,11 @@ __global__ __launch_bounds__(1024) void k_decrypt_long(DecArgs a) {
                         const uint8_t *B = Kt + 64ull * (i + 1);
                         b0 = ld16(B); b1 = ld16(B + 16); b2 = ld16(B + 32); b3 = ld16(B + 48);
                     }
+#ifndef RNSTOK_DL_PROBE_AES_ONLY          // timing probe: no HMAC chain (wrong statuses)
                     sha256_compress(h, w);
+#else
+                    h[0] ^= w[0];
+#endif
                 }
                 const uint32_t fu = (M - 64u * full) >> 4;
                 const u32x4 z = {0u, 0u, 0u, 0u};
@@ -807,7 +811,11 @@ __global__ __launch_bounds__(1024) void k_decrypt_long(DecArgs a) {
                 c[2] = nbk > 2 ? ld16(C + 32) : z;
                 c[3] = nbk > 3 ? ld16(C + 48) : z;
                 const u32x4 chain = ld16(C - 16);      // previous ciphertext block (the IV for q = 0)
+#ifndef RNSTOK_DL_PROBE_SHA_ONLY          // timing probe: no block decryption (wrong plaintext)
                 dec_quad<NR, false>(pp, c, chain, K.rk, LN, dummy);
+#else
+                pp[0] = c[0] ^ chain; pp[1] = c[1]; pp[2] = c[2]; pp[3] = c[3];
+#endif
                 st16(D, pp[0]);
                 if (nbk > 1) st16(D + 16, pp[1]);
                 if (nbk > 2) st16(D + 32, pp[2]);

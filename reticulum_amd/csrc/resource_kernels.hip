@@ -96,6 +96,44 @@ __global__ __launch_bounds__(256) void k_map_collisions(MapArgs m) {
 
 }  // namespace
 
+// The same comparison with the workgroup's window of map hashes (its 256
+// parts and the `guard` parts before them) staged in LDS once, instead of
+// every lane reading its `guard` predecessors from memory (0.12 ms of
+// global reads per 2^20 parts at guard 224).
+constexpr uint32_t COLL_TILE = 256, COLL_LDS_GUARD_MAX = 4096;
+__global__ __launch_bounds__(COLL_TILE) void k_map_collisions_lds(MapArgs m) {
+    extern __shared__ uint32_t win[];                 // [span] hashes, then [span] resource ids
+    const uint32_t j0 = blockIdx.x * COLL_TILE, lo = j0 > m.guard ? j0 - m.guard : 0u;
+    const uint32_t hi = j0 + COLL_TILE < m.n_parts ? j0 + COLL_TILE : m.n_parts, span = hi - lo;
+    uint32_t *res = win + m.guard + COLL_TILE;
+    for (uint32_t k = threadIdx.x; k < span; k += COLL_TILE) {
+        uint32_t v;
+        __builtin_memcpy(&v, m.out + 4ull * (lo + k), 4);
+        win[k] = v;
+        res[k] = m.part_res ? m.part_res[lo + k] : 0u;
+    }
+    __syncthreads();
+    const uint32_t j = j0 + threadIdx.x;
+    if (j >= m.n_parts) return;
+    const uint32_t mine = win[j - lo], r = res[j - lo];
+    const uint32_t from = j > m.guard ? j - m.guard : 0u;
+    if (res[0] == res[span - 1]) {               // the window is one resource (parts are contiguous)
+        for (uint32_t k = from; k < j; ++k) {
+            if (win[k - lo] == mine) {
+                atomicMin(m.first_collision + r, j);
+                break;
+            }
+        }
+        return;
+    }
+    for (uint32_t k = from; k < j; ++k) {
+        if (res[k - lo] == r && win[k - lo] == mine) {
+            atomicMin(m.first_collision + r, j);
+            break;
+        }
+    }
+}
+
 hipError_t launch_map_hashes(const MapArgs &m, hipStream_t s) {
     if (m.n_parts == 0) return hipSuccess;
     const uint32_t threads = 256, grid = (m.n_parts + threads - 1) / threads;
@@ -105,7 +143,11 @@ hipError_t launch_map_hashes(const MapArgs &m, hipStream_t s) {
     e = hipMemsetAsync(m.first_collision, 0xff, 4ull * m.n_res, s);      // "no collision" = 0xffffffff
     if (e != hipSuccess) return e;
     if (m.guard == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_map_collisions, dim3(grid), dim3(threads), 0, s, m);
+    if (m.guard <= COLL_LDS_GUARD_MAX)
+        hipLaunchKernelGGL(k_map_collisions_lds, dim3((m.n_parts + COLL_TILE - 1) / COLL_TILE), dim3(COLL_TILE),
+                           8u * (m.guard + COLL_TILE), s, m);
+    else
+        hipLaunchKernelGGL(k_map_collisions, dim3(grid), dim3(threads), 0, s, m);
     return hipGetLastError();
 }
 

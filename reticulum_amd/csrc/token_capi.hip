@@ -27,6 +27,13 @@ struct rt_ctx {
     std::mutex mu;                 // serialises host-staging calls
     uint8_t *d_work = nullptr;     // host-path workspace
     uint64_t work_cap = 0;
+    // Pinned mirror of the workspace for token host calls up to STAGE_MAX
+    // bytes: the caller's arrays are gathered here and cross PCIe as one copy
+    // each way.  A pageable copy pays a driver staging round trip per array
+    // (6 of them per encrypt), which dominates a one-packet Token.encrypt.
+    uint8_t *h_stage = nullptr;
+    uint64_t stage_cap = 0;
+    bool stage_busy = false;       // a copy from h_stage may still be queued
     // Chunk counters for the token kernels' dynamic packet loop (ragged
     // uniform batches): one 64-B slot per launch, round-robin, zeroed on the
     // launch's stream.  A slot is reused after QUEUE_SLOTS launches.
@@ -187,6 +194,7 @@ void rt_destroy(rt_ctx *c) {
     hipFree(c->d_queues);
     for (auto &e : c->rec_cache) hipFree(e.second);
     hipFree(c->d_work);
+    if (c->h_stage) hipHostFree(c->h_stage);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -385,6 +393,31 @@ static int ensure_work(rt_ctx *c, uint64_t bytes) {
 
 static uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
 
+static constexpr uint64_t STAGE_MAX = 8ull << 20;
+
+// The pinned stage for a token host call of `bytes`, or null (too large, or
+// the pinned allocation failed): the caller then copies from its own pageable
+// arrays.  Called under c->mu.
+static uint8_t *stage(rt_ctx *c, uint64_t bytes) {
+    if (bytes > STAGE_MAX) return nullptr;
+    if (c->stage_busy) {           // an earlier call failed between its copy and its sync
+        if (hipStreamSynchronize(c->stream) != hipSuccess) return nullptr;
+        c->stage_busy = false;
+    }
+    if (bytes > c->stage_cap) {
+        const uint64_t cap = std::min<uint64_t>(STAGE_MAX, std::max<uint64_t>({bytes, 2 * c->stage_cap, 64ull << 10}));
+        if (c->h_stage) hipHostFree(c->h_stage);
+        c->h_stage = nullptr;
+        c->stage_cap = 0;
+        if (hipHostMalloc(&c->h_stage, cap, hipHostMallocDefault) != hipSuccess) {
+            c->h_stage = nullptr;
+            return nullptr;
+        }
+        c->stage_cap = cap;
+    }
+    return c->h_stage;
+}
+
 // ----------------------------------------------------------- ratchet trials
 
 int rt_verify_trials(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,
@@ -462,28 +495,43 @@ int rt_encrypt_host(const rt_keyset *k, const uint8_t *pt, const uint64_t *pt_of
     rt_ctx *c = k->ctx;
     std::lock_guard<std::mutex> g(c->mu);
     RT_HIP(hipSetDevice(c->device), "hipSetDevice");
-    const uint64_t o_pt = 0, o_tok = align16(o_pt + std::max<uint64_t>(pt_ext, 1)),
-                   o_iv = align16(o_tok + tok_ext), o_po = align16(o_iv + 16ull * n),
+    // inputs first, the token region last: one copy in, one copy out
+    const uint64_t o_pt = 0, o_iv = align16(o_pt + std::max<uint64_t>(pt_ext, 1)), o_po = align16(o_iv + 16ull * n),
                    o_pl = align16(o_po + 8ull * n), o_to = align16(o_pl + 4ull * n), o_ki = align16(o_to + 8ull * n),
-                   total = align16(o_ki + (key_idx ? 4ull * n : 0));
+                   o_tok = align16(o_ki + (key_idx ? 4ull * n : 0)), total = align16(o_tok + tok_ext);
     if ((rc = ensure_work(c, total))) return rc;
     uint8_t *w = c->d_work;
     hipStream_t s = c->stream;
-    if (pt_ext) RT_HIP(hipMemcpyAsync(w + o_pt, pt, pt_ext, hipMemcpyHostToDevice, s), "H2D pt");
-    if (tok_sum != tok_ext)   // gaps between tokens: keep the caller's bytes there
-        RT_HIP(hipMemcpyAsync(w + o_tok, tok, tok_ext, hipMemcpyHostToDevice, s), "H2D tok");
-    RT_HIP(hipMemcpyAsync(w + o_iv, iv, 16ull * n, hipMemcpyHostToDevice, s), "H2D iv");
-    RT_HIP(hipMemcpyAsync(w + o_po, pt_off, 8ull * n, hipMemcpyHostToDevice, s), "H2D pt_off");
-    RT_HIP(hipMemcpyAsync(w + o_pl, pt_len, 4ull * n, hipMemcpyHostToDevice, s), "H2D pt_len");
-    RT_HIP(hipMemcpyAsync(w + o_to, tok_off, 8ull * n, hipMemcpyHostToDevice, s), "H2D tok_off");
-    if (key_idx) RT_HIP(hipMemcpyAsync(w + o_ki, key_idx, 4ull * n, hipMemcpyHostToDevice, s), "H2D key_idx");
+    const bool gaps = tok_sum != tok_ext;   // gaps between tokens: keep the caller's bytes there
+    uint8_t *h = stage(c, total);
+    if (h) {
+        if (pt_ext) memcpy(h + o_pt, pt, pt_ext);
+        memcpy(h + o_iv, iv, 16ull * n);
+        memcpy(h + o_po, pt_off, 8ull * n);
+        memcpy(h + o_pl, pt_len, 4ull * n);
+        memcpy(h + o_to, tok_off, 8ull * n);
+        if (key_idx) memcpy(h + o_ki, key_idx, 4ull * n);
+        if (gaps) memcpy(h + o_tok, tok, tok_ext);
+        c->stage_busy = true;
+        RT_HIP(hipMemcpyAsync(w, h, gaps ? total : o_tok, hipMemcpyHostToDevice, s), "H2D stage");
+    } else {
+        if (pt_ext) RT_HIP(hipMemcpyAsync(w + o_pt, pt, pt_ext, hipMemcpyHostToDevice, s), "H2D pt");
+        if (gaps) RT_HIP(hipMemcpyAsync(w + o_tok, tok, tok_ext, hipMemcpyHostToDevice, s), "H2D tok");
+        RT_HIP(hipMemcpyAsync(w + o_iv, iv, 16ull * n, hipMemcpyHostToDevice, s), "H2D iv");
+        RT_HIP(hipMemcpyAsync(w + o_po, pt_off, 8ull * n, hipMemcpyHostToDevice, s), "H2D pt_off");
+        RT_HIP(hipMemcpyAsync(w + o_pl, pt_len, 4ull * n, hipMemcpyHostToDevice, s), "H2D pt_len");
+        RT_HIP(hipMemcpyAsync(w + o_to, tok_off, 8ull * n, hipMemcpyHostToDevice, s), "H2D tok_off");
+        if (key_idx) RT_HIP(hipMemcpyAsync(w + o_ki, key_idx, 4ull * n, hipMemcpyHostToDevice, s), "H2D key_idx");
+    }
     EncArgs a{};
     a.pt = w + o_pt; a.pt_off = (const uint64_t *)(w + o_po); a.pt_len = (const uint32_t *)(w + o_pl);
     a.key_idx = key_idx ? (const uint32_t *)(w + o_ki) : nullptr; a.iv = w + o_iv;
     a.tok = w + o_tok; a.tok_off = (const uint64_t *)(w + o_to); a.n = n;
     if ((rc = enc_common(k, a, s))) return rc;
-    RT_HIP(hipMemcpyAsync(tok, w + o_tok, tok_ext, hipMemcpyDeviceToHost, s), "D2H tok");
+    RT_HIP(hipMemcpyAsync(h ? h + o_tok : tok, w + o_tok, tok_ext, hipMemcpyDeviceToHost, s), "D2H tok");
     RT_HIP(hipStreamSynchronize(s), "stream sync");
+    c->stage_busy = false;
+    if (h) memcpy(tok, h + o_tok, tok_ext);
     return RT_OK;
 }
 
@@ -506,25 +554,49 @@ int rt_decrypt_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_
     rt_ctx *c = k->ctx;
     std::lock_guard<std::mutex> g(c->mu);
     RT_HIP(hipSetDevice(c->device), "hipSetDevice");
-    const uint64_t o_tok = 0, o_pt = align16(std::max<uint64_t>(tok_ext, 1)), o_to = align16(o_pt + std::max<uint64_t>(pt_ext, 1)),
-                   o_tl = align16(o_to + 8ull * n), o_po = align16(o_tl + 4ull * n), o_ol = align16(o_po + 8ull * n),
-                   o_st = align16(o_ol + 4ull * n), o_ki = align16(o_st + 4ull * n),
-                   total = align16(o_ki + (key_idx ? 4ull * n : 0));
+    // inputs first, the outputs (plaintexts, lengths, status) last: one copy
+    // in, one copy out
+    const uint64_t o_tok = 0, o_to = align16(std::max<uint64_t>(tok_ext, 1)), o_tl = align16(o_to + 8ull * n),
+                   o_po = align16(o_tl + 4ull * n), o_ki = align16(o_po + 8ull * n),
+                   o_pt = align16(o_ki + (key_idx ? 4ull * n : 0)), o_ol = align16(o_pt + std::max<uint64_t>(pt_ext, 1)),
+                   o_st = align16(o_ol + 4ull * n), total = align16(o_st + 4ull * n);
     if ((rc = ensure_work(c, total))) return rc;
     uint8_t *w = c->d_work;
     hipStream_t s = c->stream;
-    if (tok_ext) RT_HIP(hipMemcpyAsync(w + o_tok, tok, tok_ext, hipMemcpyHostToDevice, s), "H2D tok");
-    if (pt_ext && pt_sum != pt_ext) RT_HIP(hipMemcpyAsync(w + o_pt, pt, pt_ext, hipMemcpyHostToDevice, s), "H2D pt");
-    RT_HIP(hipMemcpyAsync(w + o_to, tok_off, 8ull * n, hipMemcpyHostToDevice, s), "H2D tok_off");
-    RT_HIP(hipMemcpyAsync(w + o_tl, tok_len, 4ull * n, hipMemcpyHostToDevice, s), "H2D tok_len");
-    RT_HIP(hipMemcpyAsync(w + o_po, pt_off, 8ull * n, hipMemcpyHostToDevice, s), "H2D pt_off");
-    if (key_idx) RT_HIP(hipMemcpyAsync(w + o_ki, key_idx, 4ull * n, hipMemcpyHostToDevice, s), "H2D key_idx");
+    const bool gaps = pt_ext && pt_sum != pt_ext;   // gaps between plaintexts: keep the caller's bytes there
+    uint8_t *h = stage(c, total);
+    if (h) {
+        if (tok_ext) memcpy(h + o_tok, tok, tok_ext);
+        memcpy(h + o_to, tok_off, 8ull * n);
+        memcpy(h + o_tl, tok_len, 4ull * n);
+        memcpy(h + o_po, pt_off, 8ull * n);
+        if (key_idx) memcpy(h + o_ki, key_idx, 4ull * n);
+        if (gaps) memcpy(h + o_pt, pt, pt_ext);
+        c->stage_busy = true;
+        RT_HIP(hipMemcpyAsync(w, h, gaps ? o_ol : o_pt, hipMemcpyHostToDevice, s), "H2D stage");
+    } else {
+        if (tok_ext) RT_HIP(hipMemcpyAsync(w + o_tok, tok, tok_ext, hipMemcpyHostToDevice, s), "H2D tok");
+        if (gaps) RT_HIP(hipMemcpyAsync(w + o_pt, pt, pt_ext, hipMemcpyHostToDevice, s), "H2D pt");
+        RT_HIP(hipMemcpyAsync(w + o_to, tok_off, 8ull * n, hipMemcpyHostToDevice, s), "H2D tok_off");
+        RT_HIP(hipMemcpyAsync(w + o_tl, tok_len, 4ull * n, hipMemcpyHostToDevice, s), "H2D tok_len");
+        RT_HIP(hipMemcpyAsync(w + o_po, pt_off, 8ull * n, hipMemcpyHostToDevice, s), "H2D pt_off");
+        if (key_idx) RT_HIP(hipMemcpyAsync(w + o_ki, key_idx, 4ull * n, hipMemcpyHostToDevice, s), "H2D key_idx");
+    }
     DecArgs a{};
     a.tok = w + o_tok; a.tok_off = (const uint64_t *)(w + o_to); a.tok_len = (const uint32_t *)(w + o_tl);
     a.key_idx = key_idx ? (const uint32_t *)(w + o_ki) : nullptr; a.pt = w + o_pt;
     a.pt_off = (const uint64_t *)(w + o_po); a.out_len = (uint32_t *)(w + o_ol); a.status = (int32_t *)(w + o_st);
     a.n = n;
     if ((rc = dec_common(k, a, s))) return rc;
+    if (h) {
+        RT_HIP(hipMemcpyAsync(h + o_pt, w + o_pt, total - o_pt, hipMemcpyDeviceToHost, s), "D2H stage");
+        RT_HIP(hipStreamSynchronize(s), "stream sync");
+        c->stage_busy = false;
+        if (pt_ext) memcpy(pt, h + o_pt, pt_ext);
+        memcpy(pt_len, h + o_ol, 4ull * n);
+        memcpy(status, h + o_st, 4ull * n);
+        return RT_OK;
+    }
     if (pt_ext) RT_HIP(hipMemcpyAsync(pt, w + o_pt, pt_ext, hipMemcpyDeviceToHost, s), "D2H pt");
     RT_HIP(hipMemcpyAsync(pt_len, w + o_ol, 4ull * n, hipMemcpyDeviceToHost, s), "D2H pt_len");
     RT_HIP(hipMemcpyAsync(status, w + o_st, 4ull * n, hipMemcpyDeviceToHost, s), "D2H status");

@@ -72,16 +72,27 @@ __device__ __forceinline__ uint32_t td0(const uint8_t *inv, uint32_t x) {
 
 template <bool DEC>
 __device__ void fill_tables(uint32_t *tab, const uint8_t *sbox, const uint8_t *inv) {
-    // ≈5-9 µs per launch on c2 (a build that skips it: encrypt 0.888 -> 0.879 ms)
-    // regions 0,1: 32768 dwords; dword d -> region d>>14, row (d>>6)&255, table (d>>5)&1
-    for (uint32_t d = threadIdx.x; d < 32768u; d += blockDim.x) {
-        uint32_t x = (d >> 6) & 255u, t = ((d >> 14) << 1) | ((d >> 5) & 1u);
-        uint32_t v = DEC ? td0(inv, x) : te0(sbox, x);
-        tab[d] = rotl(v, 8 * (int)t);
+    // regions 0,1: 32768 dwords; dword d -> region d>>14, row (d>>6)&255,
+    // table (d>>5)&1, replica d&31.  One unit = (row x, rotation t): its entry
+    // is computed once and stored to its 32 replicas, the replica order
+    // rotated by lane so each half-wave's stores hit 32 distinct banks.  (The
+    // per-dword form recomputed Td0's GF multiplies 128 times per row and
+    // cost ≈40 µs in a one-workgroup launch.)
+    const uint32_t lane = threadIdx.x & 31u;
+    for (uint32_t u = threadIdx.x; u < 1024u; u += blockDim.x) {
+        const uint32_t x = u & 255u, t = u >> 8;
+        const uint32_t v = rotl(DEC ? td0(inv, x) : te0(sbox, x), 8 * (int)t);
+        uint32_t *row = tab + ((t >> 1) << 14) + (x << 6) + ((t & 1u) << 5);
+#pragma unroll 8
+        for (uint32_t j = 0; j < 32u; ++j) row[(j + lane) & 31u] = v;
     }
     if (DEC) {
-        for (uint32_t d = threadIdx.x; d < 8192u; d += blockDim.x)
-            tab[32768u + d] = (uint32_t)inv[d >> 5] * 0x01010101u;
+        for (uint32_t x = threadIdx.x; x < 256u; x += blockDim.x) {
+            const uint32_t v = (uint32_t)inv[x] * 0x01010101u;
+            uint32_t *row = tab + 32768u + (x << 5);
+#pragma unroll 8
+            for (uint32_t j = 0; j < 32u; ++j) row[(j + lane) & 31u] = v;
+        }
     }
     __syncthreads();
 }
@@ -1093,6 +1104,12 @@ static Shape shape_for(uint32_t n, int max_threads, int n_cu) {
     uint64_t g = ((uint64_t)n + t - 1) / t;
     if (g > (uint64_t)n_cu) g = n_cu;
     if (g < 1) g = 1;
+#ifndef RNSTOK_NO_SMALL_FILL
+    // One workgroup (up to 64 packets, e.g. a single Token.encrypt): widen it
+    // so the LDS table image is written by 512 threads, not 64 (the extra
+    // waves find no packet and leave after fill_tables).
+    if (g == 1 && t < 512 && max_threads >= 512) t = 512;
+#endif
     return {(int)g, (int)t};
 }
 

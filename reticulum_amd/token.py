@@ -34,6 +34,8 @@ AES_256_CBC = _Mode("AES_256_CBC")
 
 TOKEN_OVERHEAD = 48
 
+_OFF0 = ctypes.byref(ctypes.c_uint64(0))   # the offset array of a one-record call (read-only)
+
 
 def token_len(pt_len):
     """len(token) for a plaintext of pt_len bytes (Token.py:96-97, PKCS7.py:35-39)."""
@@ -279,9 +281,17 @@ class Token:
             self._keyset = KeySet(self._key, device=self._device)
         return self._keyset
 
+    # One packet per call, as Identity/Link call Token: the host entry points
+    # with n = 1 on ctypes scalars and the caller's bytes (no Packed arrays:
+    # building them cost ≈30-40 µs of Python per call).
     def _decrypt_one(self, token):
-        out, status, detail = self.keyset._decrypt_raw(Packed.from_list([token]))
-        return int(status[0]), out, int(detail[0])
+        ks = self.keyset
+        L = len(token)
+        out = ctypes.create_string_buffer(max(L - 48, 1))
+        olen, st = ctypes.c_uint32(0), ctypes.c_int32(0)
+        _native.check(ks._lib.rt_decrypt_host(ks._ptr, token, _OFF0, ctypes.byref(ctypes.c_uint32(L)), None, out,
+                                              _OFF0, ctypes.byref(olen), ctypes.byref(st), 1))
+        return st.value, out, olen.value
 
     def verify_hmac(self, token):                               # Token.py:77-84
         if len(token) <= 32:
@@ -292,8 +302,12 @@ class Token:
     def encrypt(self, data=None):                               # Token.py:87-97
         if not isinstance(data, bytes):
             raise TypeError("Token plaintext input must be bytes")
-        iv = np.frombuffer(os.urandom(16), dtype=np.uint8)
-        return self.keyset.encrypt_batch(Packed.from_list([data]), ivs=iv)[0]
+        ks = self.keyset
+        n = len(data)
+        out = ctypes.create_string_buffer(token_len(n))
+        _native.check(ks._lib.rt_encrypt_host(ks._ptr, data, _OFF0, ctypes.byref(ctypes.c_uint32(n)), None,
+                                              os.urandom(16), out, _OFF0, 1))      # fresh IV, Token.py:89
+        return out.raw
 
     def decrypt(self, token=None):                              # Token.py:100-114
         if not isinstance(token, bytes):
@@ -302,7 +316,7 @@ class Token:
             raise ValueError("Cannot verify HMAC on token of only " + str(len(token)) + " bytes")
         st, out, n = self._decrypt_one(token)
         if st == RT_ST_OK:
-            return out[0]
+            return out.raw[:n]
         raise ValueError(status_message(st, len(token), n))
 
     # batch extensions ---------------------------------------------------

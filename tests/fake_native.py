@@ -16,6 +16,12 @@ from oracle import ctoken
 def _arr(p, dtype, n):
     if p is None:
         return None
+    if isinstance(p, bytes):                      # Token's one-packet calls pass bytes,
+        return np.frombuffer(p, dtype=dtype)      # ctypes buffers and byref() scalars
+    if isinstance(p, ctypes.Array):
+        return np.frombuffer(p, dtype=dtype)
+    if type(p).__name__ == "CArgObject":
+        return np.frombuffer(p._obj, dtype=dtype)
     addr = p.value if isinstance(p, ctypes.c_void_p) else int(p)
     if not addr or n == 0:
         return np.zeros(0, dtype=dtype)

@@ -9,9 +9,12 @@
 // midstates computed once.  With 32-byte ikm, 16-byte salt, no context and a
 // 64-byte output that is 10 SHA-256 compressions per lane.
 //
-// The messages are assembled word by word from byte loads (global memory is
-// read once per byte; the previous block T_{i-1} comes from registers), so
-// any lengths work; this is VALU-bound like the token MAC.
+// The generic instance assembles the messages word by word from byte loads
+// (global memory is read once per byte; the previous block T_{i-1} comes from
+// registers), so any lengths work.  The common shape (ikm and salt whole
+// 4-byte words, ikm <= 52 bytes so PRK's message is one block, no context)
+// takes the FAST instance: dword loads and the padded blocks written as
+// constants.  Both are VALU-bound like the token MAC.
 #include "token_device.h"
 #include "token_launch.h"
 
@@ -72,6 +75,12 @@ __device__ __forceinline__ void hmac_midstates(const uint32_t key[16], uint32_t 
     sha256_compress(ho, wo);
 }
 
+// big-endian word at a 4-byte aligned address (FAST instance only)
+__device__ __forceinline__ uint32_t ld_be32(const uint8_t *p) {
+    return bswap(*(const uint32_t *)__builtin_assume_aligned(p, 4));
+}
+
+template <bool FAST>
 __global__ __launch_bounds__(256) void k_hkdf(HkdfArgs a) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
@@ -81,7 +90,10 @@ __global__ __launch_bounds__(256) void k_hkdf(HkdfArgs a) {
     uint32_t key[16];
     const uint32_t sl = a.salt ? a.salt_len : 0u;
     const uint8_t *salt = a.salt ? a.salt + (uint64_t)i * a.salt_stride : nullptr;
-    if (sl > 64u) {                                   // HMAC.py: long keys are hashed first
+    if (FAST) {                                       // sl % 4 == 0, sl <= 64
+#pragma unroll
+        for (int k = 0; k < 16; ++k) key[k] = 4u * k < sl ? ld_be32(salt + 4 * k) : 0u;
+    } else if (sl > 64u) {                            // HMAC.py: long keys are hashed first
         uint32_t d[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) d[k] = SHA_IV[k];
@@ -104,7 +116,17 @@ __global__ __launch_bounds__(256) void k_hkdf(HkdfArgs a) {
     hmac_midstates(key, hi, ho);
 #pragma unroll
     for (int k = 0; k < 8; ++k) inner[k] = hi[k];
-    sha_msg(inner, 64u, nullptr, 0u, ikm, a.ikm_len, -1);
+    if (FAST) {                                       // ikm_len % 4 == 0, ikm_len <= 52: one block
+        uint32_t w[16];
+#pragma unroll
+        for (int k = 0; k < 14; ++k)
+            w[k] = 4u * k < a.ikm_len ? ld_be32(ikm + 4 * k) : (4u * k == a.ikm_len ? 0x80000000u : 0u);
+        w[14] = 0u;
+        w[15] = (64u + a.ikm_len) * 8u;
+        sha256_compress(inner, w);
+    } else {
+        sha_msg(inner, 64u, nullptr, 0u, ikm, a.ikm_len, -1);
+    }
     hmac_outer(prk, inner, ho);                      // PRK = HMAC(salt, ikm)  (HKDF.py:51)
 #pragma unroll
     for (int k = 0; k < 16; ++k) key[k] = k < 8 ? prk[k] : 0u;
@@ -115,7 +137,24 @@ __global__ __launch_bounds__(256) void k_hkdf(HkdfArgs a) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) inner[k] = hi[k];
         // T_blk = HMAC(PRK, T_{blk-1} || context || (blk+1) % 256)  (HKDF.py:56-60)
-        sha_msg(inner, 64u, t, blk ? 8u : 0u, a.context, a.context_len, (int)((blk + 1u) & 255u));
+        if (FAST) {                                   // T_{blk-1} (32 B, none for blk 0) || counter byte
+            const uint32_t ctr = (((blk + 1u) & 255u) << 24) | 0x00800000u;
+            uint32_t w[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) w[k] = 0u;
+            if (blk) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) w[k] = t[k];
+                w[8] = ctr;
+                w[15] = (64u + 33u) * 8u;
+            } else {
+                w[0] = ctr;
+                w[15] = (64u + 1u) * 8u;
+            }
+            sha256_compress(inner, w);
+        } else {
+            sha_msg(inner, 64u, t, blk ? 8u : 0u, a.context, a.context_len, (int)((blk + 1u) & 255u));
+        }
         hmac_outer(t, inner, ho);
         const uint32_t take = a.length - done < 32u ? a.length - done : 32u;
         if (take == 32u) {
@@ -139,7 +178,18 @@ __global__ __launch_bounds__(256) void k_hkdf(HkdfArgs a) {
 hipError_t launch_hkdf(const HkdfArgs &a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
     const uint32_t threads = 256;
-    hipLaunchKernelGGL(k_hkdf, dim3((a.n + threads - 1) / threads), dim3(threads), 0, s, a);
+    const auto aligned4 = [](const uint8_t *p, uint64_t stride) { return (((uintptr_t)p | stride) & 3u) == 0; };
+    const bool fast = a.context_len == 0 && a.ikm_len % 4u == 0 && a.ikm_len <= 52u && aligned4(a.ikm, a.ikm_stride) &&
+                      (a.salt == nullptr || (a.salt_len % 4u == 0 && a.salt_len <= 64u && aligned4(a.salt, a.salt_stride)));
+#ifdef RNSTOK_NO_FAST_HKDF
+    const bool use_fast = false && fast;
+#else
+    const bool use_fast = fast;
+#endif
+    if (use_fast)
+        hipLaunchKernelGGL(k_hkdf<true>, dim3((a.n + threads - 1) / threads), dim3(threads), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_hkdf<false>, dim3((a.n + threads - 1) / threads), dim3(threads), 0, s, a);
     return hipGetLastError();
 }
 

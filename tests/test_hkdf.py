@@ -99,7 +99,8 @@ def test_gpu_hkdf_golden(golden_hkdf):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("salt_len,ctx_len,length", [(16, 0, 64), (0, 0, 32), (100, 30, 200), (64, 1, 33)])
+@pytest.mark.parametrize("salt_len,ctx_len,length", [(16, 0, 64), (0, 0, 32), (100, 30, 200), (64, 1, 33),
+                                                    (64, 0, 64), (20, 0, 100), (18, 0, 64)])
 def test_gpu_hkdf_device_batch_vs_oracle(salt_len, ctx_len, length):
     import torch
     from reticulum_amd import device
@@ -116,6 +117,31 @@ def test_gpu_hkdf_device_batch_vs_oracle(salt_len, ctx_len, length):
         ref = ctoken.hkdf(length, ikm[i].tobytes(), None if salt is None else salt[i].tobytes(), ctxb)
         assert got[i].tobytes() == ref, i
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ikm_len,ikm_stride", [(0, 4), (4, 4), (52, 52), (53, 53), (56, 56), (32, 34), (48, 64)])
+def test_gpu_hkdf_ikm_shapes_vs_oracle(ikm_len, ikm_stride):
+    """Both kernel instances: whole-word, <= 52-byte ikm at 4-aligned strides
+    takes the FAST instance (dword loads, one-block PRK message); 53/56 bytes
+    and the 34-byte stride take the generic byte-load instance."""
+    import torch
+    from reticulum_amd import _native
+    rng = np.random.Generator(np.random.PCG64(1000 + ikm_len * 3 + ikm_stride))
+    n = 2000
+    ikm = torch.from_numpy(rng.integers(0, 256, n * ikm_stride + 1, dtype=np.uint8)).cuda()
+    salt = torch.from_numpy(rng.integers(0, 256, (n, 16), dtype=np.uint8)).cuda()
+    out = torch.zeros((n, 64), dtype=torch.uint8, device="cuda")
+    lib = _native.load()
+    ctx = _native.context(0)
+    rc = lib.rt_hkdf(ctx, ikm.data_ptr(), ikm_stride, ikm_len, salt.data_ptr(), 16, 16, None, 0,
+                     out.data_ptr(), 64, 64, n, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    got, ih, sh = out.cpu().numpy(), ikm.cpu().numpy(), salt.cpu().numpy()
+    for i in list(range(0, n, 89)) + [n - 1]:
+        ref = ctoken.hkdf(64, ih[i * ikm_stride:i * ikm_stride + ikm_len].tobytes(), sh[i].tobytes(), None)
+        assert got[i].tobytes() == ref, i
 
 @pytest.mark.gpu
 def test_gpu_derived_keyset_identity_kat(golden_hkdf, golden):

@@ -162,7 +162,10 @@ int rt_decrypt_host(const rt_keyset *ks, const uint8_t *tok, const uint64_t *tok
  * ikm + i*ikm_stride (ikm_len bytes; 0 is allowed, as b"" is in the
  * reference), salt + i*salt_stride (salt_len bytes; salt NULL or salt_len 0
  * means the reference's default of 32 zero bytes, HKDF.py:45-46; salts over
- * 64 bytes are hashed first as HMAC.py does with long keys), a context shared
+ * 64 bytes are hashed first as HMAC.py does with long keys; salt_stride 0
+ * shares one salt row across all items, as Identity.encrypt does for packets
+ * to one identity, and the salt's HMAC midstates are then computed once per
+ * lane rather than once per item), a context shared
  * by all items (NULL / 0: empty, HKDF.py:48-49); `length` >= 1 output bytes
  * are written at out + i*out_stride (length 0 is RT_E_INVAL, HKDF.py:40-41).
  * Output blocks past 255 wrap the counter byte exactly as HKDF.py:60 does.

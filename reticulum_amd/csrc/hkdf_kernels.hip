@@ -80,16 +80,14 @@ __device__ __forceinline__ uint32_t ld_be32(const uint8_t *p) {
     return bswap(*(const uint32_t *)__builtin_assume_aligned(p, 4));
 }
 
+// HMAC(salt, .) ipad / opad midstates for key row i.
 template <bool FAST>
-__global__ __launch_bounds__(256) void k_hkdf(HkdfArgs a) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
-    const uint8_t *ikm = a.ikm + (uint64_t)i * a.ikm_stride;
+__device__ __forceinline__ void salt_midstates(const HkdfArgs &a, uint64_t i, uint32_t hi[8], uint32_t ho[8]) {
     // HMAC key = salt; None / empty salt -> 32 zero bytes (HKDF.py:45-46), which
     // zero-pads to the same 64-byte block as an empty key.
     uint32_t key[16];
     const uint32_t sl = a.salt ? a.salt_len : 0u;
-    const uint8_t *salt = a.salt ? a.salt + (uint64_t)i * a.salt_stride : nullptr;
+    const uint8_t *salt = a.salt ? a.salt + i * a.salt_stride : nullptr;
     if (FAST) {                                       // sl % 4 == 0, sl <= 64
 #pragma unroll
         for (int k = 0; k < 16; ++k) key[k] = 4u * k < sl ? ld_be32(salt + 4 * k) : 0u;
@@ -112,64 +110,89 @@ __global__ __launch_bounds__(256) void k_hkdf(HkdfArgs a) {
             key[k] = v;
         }
     }
-    uint32_t hi[8], ho[8], inner[8], prk[8];
     hmac_midstates(key, hi, ho);
+}
+
+// SHARED: one salt row for every key (salt_stride 0: a batch to one identity,
+// Identity.py:837-846, salt = the identity hash).  Its midstates are then
+// computed once per lane and reused over the lane's keys (grid-stride loop).
+template <bool FAST, bool SHARED>
+__global__ __launch_bounds__(256) void k_hkdf(HkdfArgs a) {
+    const uint64_t first = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t step = SHARED ? (uint64_t)gridDim.x * blockDim.x : (uint64_t)a.n;   // else one key per lane
+    if (first >= a.n) return;
+    uint32_t shi[8], sho[8];
+    if (SHARED) salt_midstates<FAST>(a, 0, shi, sho);
+    for (uint64_t i = first; i < a.n; i += step) {
+        const uint8_t *ikm = a.ikm + i * a.ikm_stride;
+        uint32_t hi[8], ho[8], inner[8], prk[8];
+        if (SHARED) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) inner[k] = hi[k];
-    if (FAST) {                                       // ikm_len % 4 == 0, ikm_len <= 52: one block
-        uint32_t w[16];
-#pragma unroll
-        for (int k = 0; k < 14; ++k)
-            w[k] = 4u * k < a.ikm_len ? ld_be32(ikm + 4 * k) : (4u * k == a.ikm_len ? 0x80000000u : 0u);
-        w[14] = 0u;
-        w[15] = (64u + a.ikm_len) * 8u;
-        sha256_compress(inner, w);
-    } else {
-        sha_msg(inner, 64u, nullptr, 0u, ikm, a.ikm_len, -1);
-    }
-    hmac_outer(prk, inner, ho);                      // PRK = HMAC(salt, ikm)  (HKDF.py:51)
-#pragma unroll
-    for (int k = 0; k < 16; ++k) key[k] = k < 8 ? prk[k] : 0u;
-    hmac_midstates(key, hi, ho);
-    uint32_t t[8];
-    uint8_t *out = a.out + (uint64_t)i * a.out_stride;
-    for (uint32_t blk = 0, done = 0; done < a.length; ++blk) {
+            for (int k = 0; k < 8; ++k) {
+                hi[k] = shi[k];
+                ho[k] = sho[k];
+            }
+        } else {
+            salt_midstates<FAST>(a, i, hi, ho);
+        }
+        uint32_t key[16];
 #pragma unroll
         for (int k = 0; k < 8; ++k) inner[k] = hi[k];
-        // T_blk = HMAC(PRK, T_{blk-1} || context || (blk+1) % 256)  (HKDF.py:56-60)
-        if (FAST) {                                   // T_{blk-1} (32 B, none for blk 0) || counter byte
-            const uint32_t ctr = (((blk + 1u) & 255u) << 24) | 0x00800000u;
+        if (FAST) {                                       // ikm_len % 4 == 0, ikm_len <= 52: one block
             uint32_t w[16];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) w[k] = 0u;
-            if (blk) {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) w[k] = t[k];
-                w[8] = ctr;
-                w[15] = (64u + 33u) * 8u;
-            } else {
-                w[0] = ctr;
-                w[15] = (64u + 1u) * 8u;
-            }
+            for (int k = 0; k < 14; ++k)
+                w[k] = 4u * k < a.ikm_len ? ld_be32(ikm + 4 * k) : (4u * k == a.ikm_len ? 0x80000000u : 0u);
+            w[14] = 0u;
+            w[15] = (64u + a.ikm_len) * 8u;
             sha256_compress(inner, w);
         } else {
-            sha_msg(inner, 64u, t, blk ? 8u : 0u, a.context, a.context_len, (int)((blk + 1u) & 255u));
+            sha_msg(inner, 64u, nullptr, 0u, ikm, a.ikm_len, -1);
         }
-        hmac_outer(t, inner, ho);
-        const uint32_t take = a.length - done < 32u ? a.length - done : 32u;
-        if (take == 32u) {
-            st16(out + done, u32x4{bswap(t[0]), bswap(t[1]), bswap(t[2]), bswap(t[3])});
-            st16(out + done + 16, u32x4{bswap(t[4]), bswap(t[5]), bswap(t[6]), bswap(t[7])});
-        } else {
-            for (uint32_t j = 0; j < take; ++j) {
-                uint32_t wv = t[0];
+        hmac_outer(prk, inner, ho);                      // PRK = HMAC(salt, ikm)  (HKDF.py:51)
 #pragma unroll
-                for (int k = 1; k < 8; ++k)
-                    if ((j >> 2) == (uint32_t)k) wv = t[k];
-                out[done + j] = (uint8_t)(wv >> (24u - 8u * (j & 3u)));
+        for (int k = 0; k < 16; ++k) key[k] = k < 8 ? prk[k] : 0u;
+        hmac_midstates(key, hi, ho);
+        uint32_t t[8];
+        uint8_t *out = a.out + (uint64_t)i * a.out_stride;
+        for (uint32_t blk = 0, done = 0; done < a.length; ++blk) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) inner[k] = hi[k];
+            // T_blk = HMAC(PRK, T_{blk-1} || context || (blk+1) % 256)  (HKDF.py:56-60)
+            if (FAST) {                                   // T_{blk-1} (32 B, none for blk 0) || counter byte
+                const uint32_t ctr = (((blk + 1u) & 255u) << 24) | 0x00800000u;
+                uint32_t w[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) w[k] = 0u;
+                if (blk) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) w[k] = t[k];
+                    w[8] = ctr;
+                    w[15] = (64u + 33u) * 8u;
+                } else {
+                    w[0] = ctr;
+                    w[15] = (64u + 1u) * 8u;
+                }
+                sha256_compress(inner, w);
+            } else {
+                sha_msg(inner, 64u, t, blk ? 8u : 0u, a.context, a.context_len, (int)((blk + 1u) & 255u));
             }
+            hmac_outer(t, inner, ho);
+            const uint32_t take = a.length - done < 32u ? a.length - done : 32u;
+            if (take == 32u) {
+                st16(out + done, u32x4{bswap(t[0]), bswap(t[1]), bswap(t[2]), bswap(t[3])});
+                st16(out + done + 16, u32x4{bswap(t[4]), bswap(t[5]), bswap(t[6]), bswap(t[7])});
+            } else {
+                for (uint32_t j = 0; j < take; ++j) {
+                    uint32_t wv = t[0];
+#pragma unroll
+                    for (int k = 1; k < 8; ++k)
+                        if ((j >> 2) == (uint32_t)k) wv = t[k];
+                    out[done + j] = (uint8_t)(wv >> (24u - 8u * (j & 3u)));
+                }
+            }
+            done += take;
         }
-        done += take;
     }
 }
 
@@ -186,10 +209,23 @@ hipError_t launch_hkdf(const HkdfArgs &a, hipStream_t s) {
 #else
     const bool use_fast = fast;
 #endif
-    if (use_fast)
-        hipLaunchKernelGGL(k_hkdf<true>, dim3((a.n + threads - 1) / threads), dim3(threads), 0, s, a);
+    // a shared salt row: 1024 x 256 lanes (4 waves per SIMD on 256 CUs), each
+    // computing the salt's midstates once for its n / 262144 keys
+#ifdef RNSTOK_NO_SHARED_SALT
+    const bool shared = false;
+#else
+    const bool shared = a.salt != nullptr && a.salt_stride == 0 && a.n > 1;
+#endif
+    const uint64_t blocks = ((uint64_t)a.n + threads - 1) / threads;
+    const dim3 grid((unsigned)(shared && blocks > 1024u ? 1024u : blocks));
+    if (use_fast && shared)
+        hipLaunchKernelGGL((k_hkdf<true, true>), grid, dim3(threads), 0, s, a);
+    else if (use_fast)
+        hipLaunchKernelGGL((k_hkdf<true, false>), grid, dim3(threads), 0, s, a);
+    else if (shared)
+        hipLaunchKernelGGL((k_hkdf<false, true>), grid, dim3(threads), 0, s, a);
     else
-        hipLaunchKernelGGL(k_hkdf<false>, dim3((a.n + threads - 1) / threads), dim3(threads), 0, s, a);
+        hipLaunchKernelGGL((k_hkdf<false, false>), grid, dim3(threads), 0, s, a);
     return hipGetLastError();
 }
 

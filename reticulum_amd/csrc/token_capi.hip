@@ -792,7 +792,8 @@ int rt_hkdf_host(rt_ctx *c, const uint8_t *ikm, uint64_t ikm_stride, uint32_t ik
     if (!salt) salt_len = 0;
     if (!context) context_len = 0;
     // packed copies on the device: ikm n x ikm_len, salt n x salt_len, context, out n x length
-    const uint64_t b_ikm = (uint64_t)n * ikm_len, b_salt = (uint64_t)n * salt_len, b_out = (uint64_t)n * length;
+    const uint64_t b_ikm = (uint64_t)n * ikm_len, b_salt = (salt_stride ? (uint64_t)n : 1ull) * salt_len,
+                   b_out = (uint64_t)n * length;   // salt_stride 0: one shared salt row
     const uint64_t o_ikm = 0, o_salt = align16(o_ikm + b_ikm), o_ctx = align16(o_salt + b_salt),
                    o_out = align16(o_ctx + context_len), total = align16(o_out + b_out);
     std::lock_guard<std::mutex> g(c->mu);
@@ -803,10 +804,11 @@ int rt_hkdf_host(rt_ctx *c, const uint8_t *ikm, uint64_t ikm_stride, uint32_t ik
     if (b_ikm)
         RT_HIP(hipMemcpy2DAsync(w + o_ikm, ikm_len, ikm, ikm_stride, ikm_len, n, hipMemcpyHostToDevice, s), "H2D ikm");
     if (b_salt)
-        RT_HIP(hipMemcpy2DAsync(w + o_salt, salt_len, salt, salt_stride, salt_len, n, hipMemcpyHostToDevice, s),
+        RT_HIP(hipMemcpy2DAsync(w + o_salt, salt_len, salt, salt_stride ? salt_stride : salt_len, salt_len,
+                                salt_stride ? n : 1u, hipMemcpyHostToDevice, s),
                "H2D salt");
     if (context_len) RT_HIP(hipMemcpyAsync(w + o_ctx, context, context_len, hipMemcpyHostToDevice, s), "H2D context");
-    const HkdfArgs a = hkdf_args(w + o_ikm, ikm_len, ikm_len, b_salt ? w + o_salt : nullptr, salt_len, salt_len,
+    const HkdfArgs a = hkdf_args(w + o_ikm, ikm_len, ikm_len, b_salt ? w + o_salt : nullptr, salt_stride ? salt_len : 0, salt_len,
                                  context_len ? w + o_ctx : nullptr, context_len, w + o_out, length, length, n);
     RT_HIP(launch_hkdf(a, s), "hkdf launch");
     RT_HIP(hipMemcpy2DAsync(out, out_stride, w + o_out, length, length, n, hipMemcpyDeviceToHost, s), "D2H out");

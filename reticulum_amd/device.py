@@ -34,6 +34,15 @@ def _p_rows(t):
     return t.data_ptr()
 
 
+def _p_salt(t):
+    """Salt rows: contiguous (n, S), or one row broadcast to n
+    (`salt[:1].expand(n, S)`, row stride 0: a batch to one identity)."""
+    if t is not None and t.dim() == 2 and t.shape[0] > 1 and t.stride(0) == 0 and \
+            (t.shape[1] <= 1 or t.stride(1) == 1) and t.is_cuda:
+        return t.data_ptr()
+    return _p(t)
+
+
 def _stream(stream):
     s = stream if stream is not None else torch.cuda.current_stream()
     return s.cuda_stream
@@ -126,7 +135,8 @@ def decrypt(ks: KeySet, tok, tok_off, tok_len, pt, pt_off, out_len, status, key_
 
 def hkdf(ikm, out, salt=None, context=None, stream=None):
     """HKDF-SHA256 over device rows (RNS/Cryptography/HKDF.py:35-62): ikm
-    (n, L) uint8, salt (n, S) uint8 or None (the reference's 32 zero bytes),
+    (n, L) uint8, salt (n, S) uint8 or None (the reference's 32 zero bytes;
+    one row expanded to (n, S) is shared, its HMAC midstates computed once),
     context a (C,) uint8 device tensor or None, out (n, length) uint8 with
     length = out.shape[1] >= 1.  Row i of out = hkdf(length, ikm[i], salt[i],
     context)."""
@@ -137,7 +147,7 @@ def hkdf(ikm, out, salt=None, context=None, stream=None):
     length = out.shape[1]
     lib = _native.load()
     ctx = _native.context(out.device.index)
-    _native.check(lib.rt_hkdf(ctx, _p(ikm), ikm.stride(0), ikm.shape[1], _p(salt),
+    _native.check(lib.rt_hkdf(ctx, _p(ikm), ikm.stride(0), ikm.shape[1], _p_salt(salt),
                               salt.stride(0) if salt is not None else 0, salt.shape[1] if salt is not None else 0,
                               _p(context), context.numel() if context is not None else 0, _p(out), out.stride(0),
                               length, n, _stream(stream)))
@@ -151,7 +161,7 @@ def derive_keyset(ikm, salt=None, context=None, key_len=64, stream=None):
     n = ikm.shape[0]
     lib = _native.load()
     ctx = _native.context(ikm.device.index)
-    h = lib.rt_keyset_create_hkdf(ctx, _p(ikm), ikm.stride(0), ikm.shape[1], _p(salt),
+    h = lib.rt_keyset_create_hkdf(ctx, _p(ikm), ikm.stride(0), ikm.shape[1], _p_salt(salt),
                                   salt.stride(0) if salt is not None else 0, salt.shape[1] if salt is not None else 0,
                                   _p(context), context.numel() if context is not None else 0, key_len, n,
                                   _stream(stream))

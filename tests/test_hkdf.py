@@ -143,6 +143,48 @@ def test_gpu_hkdf_ikm_shapes_vs_oracle(ikm_len, ikm_stride):
         ref = ctoken.hkdf(64, ih[i * ikm_stride:i * ikm_stride + ikm_len].tobytes(), sh[i].tobytes(), None)
         assert got[i].tobytes() == ref, i
 
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("salt_len,n", [(16, 70000), (16, 1), (18, 3000), (100, 3000)])
+def test_gpu_hkdf_shared_salt_vs_oracle(salt_len, n):
+    """salt_stride 0 (one salt row for every key, Identity.py:837-846 to one
+    identity): the grid-stride instance computes the salt's midstates once per
+    lane.  Also through rt_hkdf_host, which copies the one salt row."""
+    import torch
+    from reticulum_amd import device
+    rng = np.random.Generator(np.random.PCG64(7000 + salt_len + n))
+    ikm = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    salt = rng.integers(0, 256, (1, salt_len), dtype=np.uint8)
+    out = torch.zeros((n, 64), dtype=torch.uint8, device="cuda")
+    device.hkdf(torch.from_numpy(ikm).cuda(), out, torch.from_numpy(salt).cuda().expand(n, salt_len))
+    got = out.cpu().numpy()
+    for i in sorted(set(list(range(0, n, max(1, n // 40))) + [n - 1])):
+        assert got[i].tobytes() == ctoken.hkdf(64, ikm[i].tobytes(), salt[0].tobytes(), None), i
+    from reticulum_amd import _native
+    host = np.zeros((n, 64), dtype=np.uint8)
+    rc = _native.load().rt_hkdf_host(_native.context(0), ikm.ctypes.data, 32, 32, salt.ctypes.data, 0, salt_len,
+                                     None, 0, host.ctypes.data, 64, 64, n)
+    assert rc == 0 and np.array_equal(host, got)
+
+
+@pytest.mark.gpu
+def test_gpu_hkdf_shared_salt_grid_stride():
+    """600000 keys over the 1024 x 256-lane grid: lanes derive 2 or 3 keys."""
+    import torch
+    from reticulum_amd import device
+    n = 600000
+    g = torch.Generator(device="cuda").manual_seed(5)
+    ikm = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device="cuda", generator=g)
+    salt = torch.randint(0, 256, (1, 16), dtype=torch.uint8, device="cuda", generator=g)
+    out = torch.zeros((n, 64), dtype=torch.uint8, device="cuda")
+    ref = torch.zeros((n, 64), dtype=torch.uint8, device="cuda")
+    device.hkdf(ikm, out, salt.expand(n, 16))
+    device.hkdf(ikm, ref, salt.repeat(n, 1))          # per-row instance, same salt in every row
+    assert torch.equal(out, ref)
+    ih, sh, oh = ikm.cpu().numpy(), salt.cpu().numpy(), out.cpu().numpy()
+    for i in (0, 262143, 262144, 524288, n - 1):
+        assert oh[i].tobytes() == ctoken.hkdf(64, ih[i].tobytes(), sh[0].tobytes(), None), i
+
 @pytest.mark.gpu
 def test_gpu_derived_keyset_identity_kat(golden_hkdf, golden):
     """Identity.__decrypt's derivation + Token on the device: the keyset

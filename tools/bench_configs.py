@@ -90,6 +90,21 @@ def main():
         res["hkdf_ms"] = sorted(hk)[2]
         res["derive_keyset_ms"] = sorted(dk)[2]
         res["hkdf_keys_s"] = n / (res["hkdf_ms"] * 1e-3)
+        # one salt row for the whole batch (salt_stride 0): packets to one identity
+        shared = salt[:1].expand(n, 16)
+        okm2 = torch.empty_like(okm)
+        hs, ds = [], []
+        for _ in range(5):
+            e0.record()
+            device.hkdf(ikm, okm2, shared)
+            e1.record()
+            device.derive_keyset(ikm, shared)
+            e2.record()
+            torch.cuda.synchronize()
+            hs.append(e0.elapsed_time(e1))
+            ds.append(e1.elapsed_time(e2))
+        res["hkdf_shared_salt_ms"] = sorted(hs)[2]
+        res["derive_keyset_shared_salt_ms"] = sorted(ds)[2]
         pt = torch.randint(0, 256, (n, L), dtype=torch.uint8, device=dev, generator=g)
         iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
         kidx = torch.arange(n, dtype=torch.int32, device=dev)

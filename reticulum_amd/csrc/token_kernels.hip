@@ -1078,6 +1078,102 @@ __global__ __launch_bounds__(256) void k_key_setup(const uint8_t *keys, uint32_t
     rec[(REC_OPAD >> 2) + 1] = v4u{ho[4], ho[5], ho[6], ho[7]};
 }
 
+// The same records, written through LDS.  A lane's record is 34 16-B pieces at
+// a 544-B lane stride, so a direct store instruction touches 64 lines; here
+// each wave stages KS_P pieces of its 64 records per round and stores the
+// wave's records as runs of KS_P * 16 contiguous bytes (≈7 runs per store
+// instead of 64 pieces).  Records of consecutive keys are adjacent in HBM.
+constexpr int KS_P = 9, KS_PIECES = REC_WORDS / 4, KS_ROUNDS = (KS_PIECES + KS_P - 1) / KS_P;
+template <int NK>
+__global__ __launch_bounds__(256) void k_key_setup_staged(const uint8_t *keys, uint32_t n_keys, const uint8_t *sbox,
+                                                           uint32_t *rec_out) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    __shared__ uint8_t sb[256];
+    __shared__ v4u stage[4][64 * KS_P];
+    sb[threadIdx.x] = sbox[threadIdx.x];          // blockDim.x == 256
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t kbase = blockIdx.x * blockDim.x + (wave << 6);
+    const uint32_t k = kbase + lane < n_keys ? kbase + lane : n_keys - 1;   // tail lanes recompute the last key
+    constexpr int HALF = 4 * NK, NR = NK + 6, TOTAL = 4 * (NR + 1);
+    const uint8_t *key = keys + (uint64_t)k * (2 * HALF);
+    const uint8_t *ek = key + HALF;                              // sk = key[:HALF], ek = key[HALF:]  (Token.py:61-70)
+    uint32_t w[TOTAL];
+#pragma unroll
+    for (int i = 0; i < NK; ++i)
+        w[i] = (uint32_t)ek[4 * i] | ((uint32_t)ek[4 * i + 1] << 8) | ((uint32_t)ek[4 * i + 2] << 16) |
+               ((uint32_t)ek[4 * i + 3] << 24);
+    uint32_t rcon = 1;
+#pragma unroll
+    for (int i = NK; i < TOTAL; ++i) {          // aes256.py:146-175 (aes128.py for NK = 4)
+        uint32_t t = w[i - 1];
+        if (i % NK == 0) {
+            t = sub_word(sb, (t >> 8) | (t << 24)) ^ rcon;
+            rcon = xt4(rcon);
+        } else if (NK > 6 && i % NK == 4) {
+            t = sub_word(sb, t);
+        }
+        w[i] = w[i - NK] ^ t;
+    }
+    // HMAC midstates (HMAC.py:73-82): sk zero-padded to 64 B, ^0x36 / ^0x5c
+    uint32_t bi[16], bo[16], hi[8], ho[8];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        uint32_t v = 0;
+        if (4 * i < HALF)
+            v = ((uint32_t)key[4 * i] << 24) | ((uint32_t)key[4 * i + 1] << 16) | ((uint32_t)key[4 * i + 2] << 8) |
+                key[4 * i + 3];
+        bi[i] = v ^ 0x36363636u;
+        bo[i] = v ^ 0x5c5c5c5cu;
+    }
+    const uint32_t iv0[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                             0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) hi[i] = ho[i] = iv0[i];
+    sha256_compress(hi, bi);
+    sha256_compress(ho, bo);
+    v4u *st = stage[wave];
+    v4u *out = (v4u *)rec_out;
+    const uint32_t nvalid = kbase < n_keys ? (n_keys - kbase < 64u ? n_keys - kbase : 64u) : 0u;   // records this wave stores
+#pragma unroll
+    for (int r = 0; r < KS_ROUNDS; ++r) {
+#pragma unroll
+        for (int j = 0; j < KS_P; ++j) {
+            const int c = r * KS_P + j;              // piece c of the record: words 4c..4c+3
+            if (c < KS_PIECES) {
+                v4u d = {0, 0, 0, 0};
+                if (c < 15) {                        // REC_ENC: round keys
+                    if (4 * c < TOTAL) d = v4u{w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]};
+                } else if (c < 30) {                 // REC_DEC: dk[0] = rk[nr], dk[q] = InvMix(rk[nr-q]), dk[nr] = rk[0]
+                    const int q = c - 15;
+                    if (q <= NR) {
+                        const int o = 4 * (NR - q);
+                        d = (q == 0 || q == NR) ? v4u{w[o], w[o + 1], w[o + 2], w[o + 3]}
+                                                : v4u{inv_mix_word(w[o]), inv_mix_word(w[o + 1]),
+                                                      inv_mix_word(w[o + 2]), inv_mix_word(w[o + 3])};
+                    }
+                } else if (c == 30) {
+                    d = v4u{hi[0], hi[1], hi[2], hi[3]};
+                } else if (c == 31) {
+                    d = v4u{hi[4], hi[5], hi[6], hi[7]};
+                } else if (c == 32) {
+                    d = v4u{ho[0], ho[1], ho[2], ho[3]};
+                } else {
+                    d = v4u{ho[4], ho[5], ho[6], ho[7]};
+                }
+                st[lane * KS_P + j] = d;
+            }
+        }
+        __syncthreads();
+        const uint32_t NP = (KS_PIECES - r * KS_P) < KS_P ? (KS_PIECES - r * KS_P) : KS_P;   // constant once unrolled
+        for (uint32_t t = lane; t < nvalid * NP; t += 64u) {
+            const uint32_t rr = t / NP, pc = t - rr * NP;
+            out[(uint64_t)(kbase + rr) * KS_PIECES + r * KS_P + pc] = st[rr * KS_P + pc];
+        }
+        __syncthreads();
+    }
+}
+
 // --------------------------------------------------------------- launchers --
 
 // Launch shape: a persistent grid of at most one workgroup per CU (the table
@@ -1211,10 +1307,17 @@ hipError_t launch_decrypt(const DecArgs &args, int nr, int n_cu, uint32_t *spare
 }
 hipError_t launch_key_setup(const uint8_t *keys, uint32_t key_len, uint32_t n_keys, const uint8_t *sbox,
                             uint32_t *rec, hipStream_t s) {
+#ifndef RNSTOK_KS_DIRECT
+    if (key_len == 64)
+        hipLaunchKernelGGL(k_key_setup_staged<8>, dim3((n_keys + 255) / 256), dim3(256), 0, s, keys, n_keys, sbox, rec);
+    else
+        hipLaunchKernelGGL(k_key_setup_staged<4>, dim3((n_keys + 255) / 256), dim3(256), 0, s, keys, n_keys, sbox, rec);
+#else
     if (key_len == 64)
         hipLaunchKernelGGL(k_key_setup<8>, dim3((n_keys + 255) / 256), dim3(256), 0, s, keys, n_keys, sbox, rec);
     else
         hipLaunchKernelGGL(k_key_setup<4>, dim3((n_keys + 255) / 256), dim3(256), 0, s, keys, n_keys, sbox, rec);
+#endif
     return hipGetLastError();
 }
 hipError_t configure_kernels() {

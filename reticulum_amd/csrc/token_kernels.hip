@@ -1083,7 +1083,10 @@ __global__ __launch_bounds__(256) void k_key_setup(const uint8_t *keys, uint32_t
 // each wave stages KS_P pieces of its 64 records per round and stores the
 // wave's records as runs of KS_P * 16 contiguous bytes (≈7 runs per store
 // instead of 64 pieces).  Records of consecutive keys are adjacent in HBM.
-constexpr int KS_P = 9, KS_PIECES = REC_WORDS / 4, KS_ROUNDS = (KS_PIECES + KS_P - 1) / KS_P;
+#ifndef RNSTOK_KS_P
+#define RNSTOK_KS_P 12
+#endif
+constexpr int KS_P = RNSTOK_KS_P, KS_PIECES = REC_WORDS / 4, KS_ROUNDS = (KS_PIECES + KS_P - 1) / KS_P;
 template <int NK>
 __global__ __launch_bounds__(256) void k_key_setup_staged(const uint8_t *keys, uint32_t n_keys, const uint8_t *sbox,
                                                            uint32_t *rec_out) {

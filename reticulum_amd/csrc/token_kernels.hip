@@ -1081,7 +1081,7 @@ __global__ __launch_bounds__(256) void k_key_setup(const uint8_t *keys, uint32_t
 // The same records, written through LDS.  A lane's record is 34 16-B pieces at
 // a 544-B lane stride, so a direct store instruction touches 64 lines; here
 // each wave stages KS_P pieces of its 64 records per round and stores the
-// wave's records as runs of KS_P * 16 contiguous bytes (≈7 runs per store
+// wave's records as runs of KS_P * 16 contiguous bytes (≈64 / KS_P runs per store
 // instead of 64 pieces).  Records of consecutive keys are adjacent in HBM.
 #ifndef RNSTOK_KS_P
 #define RNSTOK_KS_P 12

@@ -123,10 +123,22 @@ struct Keys {
                 rk[4 * i] = v.x; rk[4 * i + 1] = v.y; rk[4 * i + 2] = v.z; rk[4 * i + 3] = v.w;
             }
         } else {
+#ifdef RNSTOK_KEYS_VGPR
+            // one key, schedule in VGPRs: a VALU op with an SGPR operand issues
+            // at half rate on gfx950 (tools/cost_probe.hip)
+#pragma unroll
+            for (int i = 0; i < NR + 1; ++i) {
+                u32x4 v = *(const u32x4 *)(rec + base + 4 * i);
+                rk[4 * i] = v.x; rk[4 * i + 1] = v.y; rk[4 * i + 2] = v.z; rk[4 * i + 3] = v.w;
+            }
+#pragma unroll
+            for (int i = 0; i < 4 * (NR + 1); ++i) asm volatile("" : "+v"(rk[i]));
+#else
             // one key for the whole launch: keep the schedule in SGPRs (VOP3
             // operands), leaving the VGPR budget to the AES/SHA chains
 #pragma unroll
             for (int i = 0; i < 4 * (NR + 1); ++i) rk[i] = __builtin_amdgcn_readfirstlane(rec[base + i]);
+#endif
         }
     }
 };
@@ -237,8 +249,11 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
             Sha256 S;                       // S.w: the pending SHA block (previous quad's units)
 #pragma unroll
             for (int k = 0; k < 16; ++k) S.w[k] = 0u;
-#pragma nounroll
-            for (uint32_t q = 0; q <= nq; ++q) {
+            // Quad 0 is peeled: the AES chain alone (no SHA block yet), so
+            // the loop carries its SHA rounds unconditionally (a loop that
+            // branched on q == 0 was unswitched by the compiler into one body
+            // with a scalar branch around every SHA round: 1.8 % slower, A/B).
+            auto load_quad = [&](uint32_t q) {
                 if (q < nq) {
                     x[0] = ld16(P); x[1] = ld16(P + 16); x[2] = ld16(P + 32); x[3] = ld16(P + 48);
                 } else {
@@ -247,25 +262,33 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
                         x[j] = (uint32_t)j + 1u < tb ? ld16(P + 16 * j)
                                                      : ((uint32_t)j + 1u == tb ? pad_block(P + 16 * j, rem) : z);
                 }
-                S.start(h);
-                if (q == 0u)        // no SHA block yet: the AES chain alone (a second, SHA-free copy of the
-                    enc_quad<NR, false>(c, x, prev, K.rk, LN, S);     // quad; 4 % faster than hashing zeros)
-                else
-                    enc_quad<NR, true>(c, x, prev, K.rk, LN, S);
-                // The SHA rounds' results are consumed here, in the AES
-                // chain's block: otherwise the compiler sinks the rounds
-                // past the stores below and the two chains run back to back.
-                // (A select, not a branch, for quad 0's dropped compression.)
-#pragma unroll
-                for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(S.v[k]));
-                const bool keep = q > 0u;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) h[k] += keep ? S.v[k] : 0u;
+            };
+            auto store_quad = [&](uint32_t q) {
                 const uint32_t nst = q < nq ? 4u : tb;
                 st16(C, c[0]);
                 if (nst > 1u) st16(C + 16, c[1]);
                 if (nst > 2u) st16(C + 32, c[2]);
                 if (nst > 3u) st16(C + 48, c[3]);
+            };
+            load_quad(0u);
+            enc_quad<NR, false>(c, x, prev, K.rk, LN, S);
+            store_quad(0u);
+            sha_units(S.w, prev, c[0], c[1], c[2]);
+            prev = c[3];
+            P += 64; C += 64;
+#pragma nounroll
+            for (uint32_t q = 1; q <= nq; ++q) {
+                load_quad(q);
+                S.start(h);
+                enc_quad<NR, true>(c, x, prev, K.rk, LN, S);
+                // The SHA rounds' results are consumed here, in the AES
+                // chain's block: otherwise the compiler sinks the rounds past
+                // the stores below and the two chains run back to back.
+#pragma unroll
+                for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(S.v[k]));
+#pragma unroll
+                for (int k = 0; k < 8; ++k) h[k] += S.v[k];
+                store_quad(q);
                 sha_units(S.w, prev, c[0], c[1], c[2]);
                 prev = c[3];
                 P += 64; C += 64;

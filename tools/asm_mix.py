@@ -1,0 +1,50 @@
+"""Instruction mix of a kernel's hottest basic blocks from a hipcc --save-temps .s file.
+
+  python tools/asm_mix.py <file.s> <kernel-symbol-substring> [--top N]
+
+Splits the kernel's body at labels/branches and prints, for the N largest
+blocks, the count of every mnemonic (used to price the loop body in VALU
+issue slots: half-rate ops count 2)."""
+import collections
+import re
+import sys
+
+HALF = {"v_perm_b32", "v_alignbit_b32", "v_add3_u32", "v_bfi_b32", "v_and_or_b32", "v_lshl_or_b32",
+        "v_lshlrev_b64", "v_lshrrev_b64", "v_pk_mov_b32", "v_or3_b32", "v_xad_u32", "v_lshl_add_u32",
+        "v_add_lshl_u32", "v_bfe_u32", "v_mad_u32_u24", "v_mad_u64_u32", "v_mul_lo_u32", "v_mul_hi_u32"}
+
+
+def main():
+    path, sym = sys.argv[1], sys.argv[2]
+    top = int(sys.argv[sys.argv.index("--top") + 1]) if "--top" in sys.argv else 3
+    lines = open(path).read().split("\n")
+    start = next(i for i, l in enumerate(lines) if l.startswith("_Z") and sym in l and l.rstrip().endswith(":") or
+                 (l.startswith("_Z") and sym in l.split(":")[0]))
+    end = next(i for i in range(start + 1, len(lines)) if lines[i].startswith(".Lfunc_end"))
+    blocks, cur, name = [], [], "entry"
+    for l in lines[start + 1:end]:
+        s = l.strip()
+        if not s or s.startswith(";") or s.startswith("."):
+            if re.match(r"^\.LBB\d+_\d+:", s):
+                blocks.append((name, cur)); cur, name = [], s[:-1]
+            continue
+        m = s.split()[0]
+        cur.append((m, s))
+        if m.startswith("s_cbranch") or m == "s_branch":
+            blocks.append((name, cur)); cur, name = [], name + "+"
+    blocks.append((name, cur))
+    blocks.sort(key=lambda b: -len(b[1]))
+    for name, ins in blocks[:top]:
+        c = collections.Counter(m for m, _ in ins)
+        valu = sum(v for m, v in c.items() if m.startswith("v_"))
+        slots = sum(v * (2 if m in HALF else 1) for m, v in c.items() if m.startswith("v_"))
+        sgpr_ops = sum(1 for m, s in ins if m.startswith("v_") and re.search(r",\s*s\d+|,\s*s\[", s))
+        lit = sum(1 for m, s in ins if m.startswith("v_") and re.search(r"0x[0-9a-f]{3,}", s))
+        print(f"== block {name}: {len(ins)} instr, VALU {valu}, slots(half=2) {slots}, VALU w/ SGPR operand {sgpr_ops}, "
+              f"w/ literal {lit}")
+        for m, v in c.most_common(40):
+            print(f"   {v:6d} {m}{'  (half)' if m in HALF else ''}")
+
+
+if __name__ == "__main__":
+    main()

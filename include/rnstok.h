@@ -12,6 +12,7 @@
  *                       per-call HMAC key pad HMAC.py:73-82, hoisted per key)
  *   rt_encrypt*        Token.encrypt             RNS/Cryptography/Token.py:87-97
  *   rt_decrypt*        Token.verify_hmac+decrypt RNS/Cryptography/Token.py:77-84,100-114
+ *   rt_verify*         Token.verify_hmac         RNS/Cryptography/Token.py:77-84 (no AES)
  *   rt_token_len       token size arithmetic     Token.py:50 (TOKEN_OVERHEAD) + PKCS7.py:35-39
  *   rt_hkdf*           RNS.Cryptography.hkdf     RNS/Cryptography/HKDF.py:35-62
  *   rt_map_hashes /    Resource hashmap          RNS/Resource.py:426-468 (map hashes + the
@@ -47,9 +48,16 @@
  *    ek = key[16:32], AES-128-CBC.  One keyset holds keys of one length.
  *  - IVs are supplied by the caller (16 bytes per packet), drawn from
  *    os.urandom as in Token.py:89; the library never generates IVs.
- *  - Thread safety: a context may be used from several host threads; host
- *    staging calls are serialised per context.  Device calls are re-entrant
- *    given distinct output buffers.
+ *  - Thread safety: a context may be used from several host threads.  Host
+ *    staging calls run on one of the context's staging lanes (each its own
+ *    stream, workspace and pinned buffer), so up to 4 run concurrently.
+ *    Device calls are re-entrant given distinct output buffers, from any
+ *    thread and on any streams.
+ *  - Stream ordering of key sets: a key set is built on the stream it was
+ *    created on (rt_keyset_create: a staging lane's stream), and every later
+ *    launch that reads it, on any stream, first waits for that build.
+ *    rt_keyset_destroy never blocks: the records are released once the last
+ *    launch on every stream that used them has completed.
  */
 #ifndef RNSTOK_H
 #define RNSTOK_H
@@ -131,6 +139,18 @@ int rt_decrypt_uniform(const rt_keyset *ks, const uint8_t *tok, uint64_t tok_str
                        const uint32_t *key_idx, uint8_t *pt, uint64_t pt_stride, uint32_t *pt_len,
                        int32_t *status, uint32_t n, void *stream);
 
+/* ---- device-resident batch (Token.verify_hmac over n tokens) ------------- */
+/* status[i] = RT_ST_OK when token i's last 32 bytes equal HMAC-SHA256(sk,
+ * token[:-32]), RT_ST_BAD_HMAC when they do not, RT_ST_TOO_SHORT when
+ * tok_len[i] <= 32 (Token.py:77-84: any length above 32 is hashed, whole AES
+ * blocks or not).  Runs no AES and writes nothing but the status.  DEVICE
+ * pointers; rt_verify_host takes HOST pointers and returns when `status` is
+ * filled. */
+int rt_verify(const rt_keyset *ks, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,
+              const uint32_t *key_idx, int32_t *status, uint32_t n, void *stream);
+int rt_verify_host(const rt_keyset *ks, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,
+                   const uint32_t *key_idx, int32_t *status, uint32_t n);
+
 /* ---- irregular batches: length bucketing -------------------------------- */
 /* With RT_F_SORT_BY_LENGTH the batch is first grouped by length on the device
  * (three small kernels on the same stream) so that the lanes of a wavefront
@@ -148,8 +168,8 @@ int rt_decrypt_ex(const rt_keyset *ks, const uint8_t *tok, const uint64_t *tok_o
                   int32_t *status, uint32_t n, uint32_t flags, void *workspace, void *stream);
 
 /* ---- host-buffer convenience (PCIe-inclusive path) ----------------------- */
-/* Same meaning with HOST pointers; H2D, kernel, D2H on the context's stream,
- * synchronised before return. */
+/* Same meaning with HOST pointers; H2D, kernel, D2H on a staging lane's
+ * stream, synchronised (that stream only) before return. */
 int rt_encrypt_host(const rt_keyset *ks, const uint8_t *pt, const uint64_t *pt_off, const uint32_t *pt_len,
                     const uint32_t *key_idx, const uint8_t *iv, uint8_t *tok, const uint64_t *tok_off,
                     uint32_t n);

@@ -34,6 +34,8 @@ SIGNATURES = [
     ("rt_encrypt_uniform", _int, [_vp, _vp, _u64, _u32, _vp, _vp, _vp, _u64, _u32, _vp]),
     ("rt_decrypt", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),
     ("rt_decrypt_uniform", _int, [_vp, _vp, _u64, _u32, _vp, _vp, _u64, _vp, _vp, _u32, _vp]),
+    ("rt_verify", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),
+    ("rt_verify_host", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _u32]),
     ("rt_workspace_bytes", _u64, [_u32]),
     ("rt_encrypt_ex", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp]),
     ("rt_decrypt_ex", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp]),

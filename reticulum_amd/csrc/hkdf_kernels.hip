@@ -15,6 +15,7 @@
 // 4-byte words, ikm <= 52 bytes so PRK's message is one block, no context)
 // takes the FAST instance: dword loads and the padded blocks written as
 // constants.  Both are VALU-bound like the token MAC.
+#include "keysetup_device.h"
 #include "token_device.h"
 #include "token_launch.h"
 
@@ -75,13 +76,38 @@ __device__ __forceinline__ void hmac_midstates(const uint32_t key[16], uint32_t 
     sha256_compress(ho, wo);
 }
 
+// The same, one compression at a time (no interleaving of the two chains:
+// register pressure in k_hkdf_key_setup).
+__device__ __forceinline__ void hmac_midstates_serial(const uint32_t key[16], uint32_t hi[8], uint32_t ho[8]) {
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = key[i] ^ 0x36363636u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) hi[i] = ho[i] = SHA_IV[i];
+    sha256_compress_fenced(hi, w);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = key[i] ^ 0x5c5c5c5cu;
+    sha256_compress_fenced(ho, w);
+}
+
+__device__ __forceinline__ void hmac_outer_fenced(uint32_t tag[8], const uint32_t inner[8], const uint32_t opad[8]) {
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { w[i] = inner[i]; tag[i] = opad[i]; }
+    w[8] = 0x80000000u;
+#pragma unroll
+    for (int i = 9; i < 15; ++i) w[i] = 0;
+    w[15] = (64 + 32) * 8;
+    sha256_compress_fenced(tag, w);
+}
+
 // big-endian word at a 4-byte aligned address (FAST instance only)
 __device__ __forceinline__ uint32_t ld_be32(const uint8_t *p) {
     return bswap(*(const uint32_t *)__builtin_assume_aligned(p, 4));
 }
 
 // HMAC(salt, .) ipad / opad midstates for key row i.
-template <bool FAST>
+template <bool FAST, bool FENCED = false>
 __device__ __forceinline__ void salt_midstates(const HkdfArgs &a, uint64_t i, uint32_t hi[8], uint32_t ho[8]) {
     // HMAC key = salt; None / empty salt -> 32 zero bytes (HKDF.py:45-46), which
     // zero-pads to the same 64-byte block as an empty key.
@@ -110,7 +136,10 @@ __device__ __forceinline__ void salt_midstates(const HkdfArgs &a, uint64_t i, ui
             key[k] = v;
         }
     }
-    hmac_midstates(key, hi, ho);
+    if (FENCED)
+        hmac_midstates_serial(key, hi, ho);
+    else
+        hmac_midstates(key, hi, ho);
 }
 
 // SHARED: one salt row for every key (salt_stride 0: a batch to one identity,
@@ -196,6 +225,90 @@ __global__ __launch_bounds__(256) void k_hkdf(HkdfArgs a) {
     }
 }
 
+// HKDF and key setup fused (the FAST shape: no context, ikm <= 52 B and salt
+// <= 64 B in whole aligned words): per-packet keying as Identity.encrypt /
+// __decrypt construct it (Identity.py:837-846, Token(hkdf(64, shared_key,
+// salt))).  Each lane derives its key into registers — T1 (and T2 for 64-B
+// keys) — and builds its record exactly as k_key_setup does from memory, so
+// the derived keys never reach HBM and one launch replaces two.  The loop is
+// wave-uniform (records are staged per wave); SHARED keeps the salt's
+// midstates for the lane's keys.
+template <bool SHARED, int NK>
+// 3 waves per SIMD: the 48 KiB staging area admits 3 workgroups per CU
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_hkdf_key_setup(HkdfArgs a, const uint8_t *sbox, uint32_t *rec_out) {
+    __shared__ uint8_t sb[256];
+    __shared__ u32x4 stage[4][KS_STAGE_PIECES];
+    sb[threadIdx.x] = sbox[threadIdx.x];          // blockDim.x == 256
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint32_t shi[8], sho[8];
+    if (SHARED) salt_midstates<true, true>(a, 0, shi, sho);
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t kb = (uint64_t)blockIdx.x * blockDim.x + (wave << 6); kb < a.n; kb += step) {
+        const uint32_t kbase = (uint32_t)kb;
+        const uint32_t i = kbase + lane < a.n ? kbase + lane : a.n - 1u;   // tail lanes: a copy of the last key
+        uint32_t hi[8], ho[8], inner[8], prk[8];
+        if (SHARED) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                hi[k] = shi[k];
+                ho[k] = sho[k];
+            }
+        } else {
+            salt_midstates<true, true>(a, i, hi, ho);
+        }
+        const uint8_t *ikm = a.ikm + (uint64_t)i * a.ikm_stride;
+        {
+            uint32_t w[16];
+#pragma unroll
+            for (int k = 0; k < 14; ++k)
+                w[k] = 4u * k < a.ikm_len ? ld_be32(ikm + 4 * k) : (4u * k == a.ikm_len ? 0x80000000u : 0u);
+            w[14] = 0u;
+            w[15] = (64u + a.ikm_len) * 8u;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) inner[k] = hi[k];
+            sha256_compress_fenced(inner, w);
+        }
+        hmac_outer_fenced(prk, inner, ho);                      // PRK = HMAC(salt, ikm)  (HKDF.py:51)
+        {
+            uint32_t key[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) key[k] = k < 8 ? prk[k] : 0u;
+            hmac_midstates_serial(key, hi, ho);
+        }
+        uint32_t t1[8], t2[8];
+        {                                                // T1 = HMAC(PRK, 0x01)  (HKDF.py:56-60)
+            uint32_t w[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) w[k] = 0u;
+            w[0] = 0x01800000u;
+            w[15] = (64u + 1u) * 8u;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) inner[k] = hi[k];
+            sha256_compress_fenced(inner, w);
+            hmac_outer_fenced(t1, inner, ho);
+        }
+        if (NK == 8) {                                   // T2 = HMAC(PRK, T1 || 0x02)
+            uint32_t w[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) w[k] = k < 8 ? t1[k] : 0u;
+            w[8] = 0x02800000u;
+            w[15] = (64u + 33u) * 8u;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) inner[k] = hi[k];
+            sha256_compress_fenced(inner, w);
+            hmac_outer_fenced(t2, inner, ho);
+        }
+        // key = T1 || T2 (big-endian words): sk = key[:HALF], ek = key[HALF:]  (Token.py:61-70)
+        uint32_t skw[16], ekw[NK];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) skw[k] = k < (NK == 8 ? 8 : 4) ? t1[k] : 0u;
+#pragma unroll
+        for (int k = 0; k < NK; ++k) ekw[k] = bswap(NK == 8 ? t2[k] : t1[4 + k]);
+        key_record<NK>(sb, ekw, skw, stage[wave], lane, kbase, a.n, rec_out);
+    }
+}
+
 }  // namespace
 
 hipError_t launch_hkdf(const HkdfArgs &a, hipStream_t s) {
@@ -226,6 +339,37 @@ hipError_t launch_hkdf(const HkdfArgs &a, hipStream_t s) {
         hipLaunchKernelGGL((k_hkdf<false, true>), grid, dim3(threads), 0, s, a);
     else
         hipLaunchKernelGGL((k_hkdf<false, false>), grid, dim3(threads), 0, s, a);
+    return hipGetLastError();
+}
+
+#ifndef RNSTOK_FUSED_BLOCKS_PER_CU
+#define RNSTOK_FUSED_BLOCKS_PER_CU 3      // 48 KiB of staging and 132 VGPRs: 3 workgroups of 4 waves per CU
+#endif
+hipError_t launch_hkdf_key_setup(const HkdfArgs &a, const uint8_t *sbox, uint32_t *rec, int n_cu, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+#ifdef RNSTOK_NO_FUSED_HKDF          // A/B: the two-launch path
+    return hipErrorNotSupported;
+#endif
+    const auto aligned4 = [](const uint8_t *p, uint64_t stride) { return (((uintptr_t)p | stride) & 3u) == 0; };
+    const bool fast = a.context_len == 0 && a.ikm_len % 4u == 0 && a.ikm_len <= 52u && aligned4(a.ikm, a.ikm_stride) &&
+                      (a.salt == nullptr || (a.salt_len % 4u == 0 && a.salt_len <= 64u && aligned4(a.salt, a.salt_stride)));
+    if (!fast || (a.length != 64u && a.length != 32u)) return hipErrorNotSupported;
+    const bool shared = a.salt != nullptr && a.salt_stride == 0 && a.n > 1;
+    uint64_t blocks = ((uint64_t)a.n + 255u) / 256u;
+    if (shared && blocks > (uint64_t)RNSTOK_FUSED_BLOCKS_PER_CU * (uint64_t)n_cu)
+        blocks = (uint64_t)RNSTOK_FUSED_BLOCKS_PER_CU * (uint64_t)n_cu;
+    const dim3 grid((unsigned)blocks);
+    if (a.length == 64u) {
+        if (shared)
+            hipLaunchKernelGGL((k_hkdf_key_setup<true, 8>), grid, dim3(256), 0, s, a, sbox, rec);
+        else
+            hipLaunchKernelGGL((k_hkdf_key_setup<false, 8>), grid, dim3(256), 0, s, a, sbox, rec);
+    } else {
+        if (shared)
+            hipLaunchKernelGGL((k_hkdf_key_setup<true, 4>), grid, dim3(256), 0, s, a, sbox, rec);
+        else
+            hipLaunchKernelGGL((k_hkdf_key_setup<false, 4>), grid, dim3(256), 0, s, a, sbox, rec);
+    }
     return hipGetLastError();
 }
 

@@ -19,12 +19,13 @@
 
 using namespace rnstok;
 
-struct rt_ctx {
-    int device = 0;
-    int n_cu = 0;
+// A host-staging lane: a private stream, a device workspace and a pinned
+// mirror of it.  The context keeps N_STAGERS of them, so host calls from
+// several threads (e.g. one reader thread per interface) run concurrently
+// instead of queueing on one lock; a call takes a free lane or waits for one.
+struct Stager {
+    std::mutex mu;
     hipStream_t stream = nullptr;
-    uint8_t *d_sbox = nullptr;     // 512 B: S-box || inverse S-box
-    std::mutex mu;                 // serialises host-staging calls
     uint8_t *d_work = nullptr;     // host-path workspace
     uint64_t work_cap = 0;
     // Pinned mirror of the workspace for token host calls up to STAGE_MAX
@@ -33,59 +34,79 @@ struct rt_ctx {
     // (6 of them per encrypt), which dominates a one-packet Token.encrypt.
     uint8_t *h_stage = nullptr;
     uint64_t stage_cap = 0;
-    bool stage_busy = false;       // a copy from h_stage may still be queued
-    // Chunk counters for the token kernels' dynamic packet loop (ragged
-    // uniform batches): one 64-B slot per launch, round-robin, zeroed on the
-    // launch's stream.  A slot is reused after QUEUE_SLOTS launches.
-    static constexpr uint32_t QUEUE_SLOTS = 1024;
-    uint32_t *d_queues = nullptr;
-    std::atomic<uint32_t> q_next{0};
-    // Key-record buffers of destroyed key sets, kept for the next key set of
-    // a similar size: per-packet keying (a fresh HKDF key set per batch,
-    // Identity.py:837-846) would otherwise pay a hipMalloc of n x 544 B per
-    // batch on the host timeline.  Destroy already synchronises the device, so
-    // a cached buffer is idle.
-    std::mutex rec_mu;
-    std::vector<std::pair<uint64_t, uint32_t *>> rec_cache;   // (capacity bytes, buffer)
+    bool stage_busy = false;       // a copy from h_stage may still be queued on `stream`
+};
+static constexpr int N_STAGERS = 4;
+
+// Chunk counters for the token kernels' dynamic packet loop (ragged uniform
+// batches): one 64-B slot per launch, round-robin.  A slot is handed out
+// again only after the stream of its next user waits on the event recorded
+// after its previous launch, so a counter is never zeroed or advanced while
+// an earlier launch (on any stream) may still read it.  The ring's lock is
+// held from acquire() to release(), i.e. across one memset and one launch.
+struct QueueRing final : SpareQueue {
+    static constexpr uint32_t SLOTS = 256;
+    std::mutex mu;
+    uint32_t *d = nullptr;
+    hipEvent_t ev[SLOTS] = {};
+    bool recorded[SLOTS] = {};
+    uint32_t next = 0, cur = 0;
+    uint32_t *acquire(hipStream_t s) override {
+        if (!d) return nullptr;
+        mu.lock();
+        cur = next;
+        next = (next + 1u) % SLOTS;
+        if (recorded[cur] && hipStreamWaitEvent(s, ev[cur], 0) != hipSuccess) {
+            mu.unlock();
+            return nullptr;
+        }
+        return d + 16u * cur;
+    }
+    void release(hipStream_t s) override {
+        if (hipEventRecord(ev[cur], s) == hipSuccess) recorded[cur] = true;
+        mu.unlock();
+    }
 };
 
-static constexpr size_t REC_CACHE_MAX = 4;
+struct rt_ctx {
+    int device = 0;
+    int n_cu = 0;
+    // Reclaim stream: a destroyed key set's records are freed here, after
+    // the events of their last launches (no host or device-wide sync).
+    hipStream_t stream = nullptr;
+    uint8_t *d_sbox = nullptr;     // 512 B: S-box || inverse S-box
+    // Stream-ordered pool for key records: a per-packet key set per batch
+    // (Identity.py:837-846) reuses the memory of the previous one without a
+    // hipMalloc/hipFree (both synchronise the device) on the host timeline.
+    hipMemPool_t pool = nullptr;
+    Stager stagers[N_STAGERS];
+    std::atomic<uint32_t> stager_rr{0};
+    QueueRing queues;
+};
 
-static uint32_t *rec_alloc(rt_ctx *c, uint64_t bytes, uint64_t *cap) {
-    {
-        std::lock_guard<std::mutex> g(c->rec_mu);
-        for (size_t i = 0; i < c->rec_cache.size(); ++i) {
-            const uint64_t have = c->rec_cache[i].first;
-            if (have >= bytes && have <= 2 * bytes + (1u << 20)) {
-                uint32_t *p = c->rec_cache[i].second;
-                *cap = have;
-                c->rec_cache.erase(c->rec_cache.begin() + i);
-                return p;
+// Takes a free staging lane (or waits for the caller's round-robin one).
+struct StageLock {
+    Stager *g = nullptr;
+    explicit StageLock(rt_ctx *c) {
+        const uint32_t start = c->stager_rr.fetch_add(1);
+        for (int i = 0; i < N_STAGERS; ++i) {
+            Stager &t = c->stagers[(start + i) % N_STAGERS];
+            if (t.mu.try_lock()) {
+                g = &t;
+                return;
             }
         }
+        g = &c->stagers[start % N_STAGERS];
+        g->mu.lock();
     }
-    uint32_t *p = nullptr;
-    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
-    *cap = bytes;
-    return p;
-}
+    ~StageLock() { g->mu.unlock(); }
+    StageLock(const StageLock &) = delete;
+    StageLock &operator=(const StageLock &) = delete;
+};
 
-static void rec_release(rt_ctx *c, uint32_t *p, uint64_t cap) {
-    if (!p) return;
-    uint32_t *evict = nullptr;
-    {
-        std::lock_guard<std::mutex> g(c->rec_mu);
-        c->rec_cache.emplace_back(cap, p);
-        if (c->rec_cache.size() > REC_CACHE_MAX) {
-            evict = c->rec_cache.front().second;
-            c->rec_cache.erase(c->rec_cache.begin());
-        }
-    }
-    if (evict) hipFree(evict);
-}
-
-static uint32_t *next_queue(rt_ctx *c) {
-    return c->d_queues ? c->d_queues + 16u * (c->q_next.fetch_add(1) % rt_ctx::QUEUE_SLOTS) : nullptr;
+static hipError_t rec_alloc(rt_ctx *c, uint64_t bytes, uint32_t **p, hipStream_t s) {
+    *p = nullptr;
+    return c->pool ? hipMallocFromPoolAsync((void **)p, bytes, c->pool, s) : hipMallocAsync((void **)p, bytes, s);
 }
 
 struct rt_keyset {
@@ -93,8 +114,29 @@ struct rt_keyset {
     uint32_t key_len = 0, n_keys = 0;
     int nr = 0;
     uint32_t *d_rec = nullptr;
-    uint64_t rec_cap = 0;          // bytes of d_rec (it may come from the context's cache)
+    hipStream_t home = nullptr;    // the stream the records were built on
+    hipEvent_t ready = nullptr;    // recorded on `home` after the key setup
+    // The last launch on each stream that read the records: destroy orders
+    // the free after all of them.
+    std::mutex mu;
+    std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
 };
+
+// Work enqueued on `s` from here on sees the key set's records.
+static hipError_t after_setup(const rt_keyset *k, hipStream_t s) {
+    return s == k->home ? hipSuccess : hipStreamWaitEvent(s, k->ready, 0);
+}
+// The launch just enqueued on `s` reads the records.
+static hipError_t note_use(rt_keyset *k, hipStream_t s) {
+    std::lock_guard<std::mutex> g(k->mu);
+    for (auto &u : k->uses)
+        if (u.first == s) return hipEventRecord(u.second, s);
+    hipEvent_t e = nullptr;
+    hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (r != hipSuccess) return r;
+    k->uses.emplace_back(s, e);
+    return hipEventRecord(e, s);
+}
 
 static thread_local std::string g_err;
 
@@ -137,6 +179,38 @@ static void make_sbox(uint8_t s[256], uint8_t inv[256]) {
 // (torch's default stream), never the context's private staging stream.
 static hipStream_t pick(const rt_ctx *, void *stream) { return (hipStream_t)stream; }
 
+static int ensure_work(Stager &g, uint64_t bytes);
+static uint8_t *stage(Stager &g, uint64_t bytes);
+
+// A key set whose records are allocated and built on stream s.  `build`
+// enqueues the kernel(s) that write k->d_rec.
+template <class Build>
+static rt_keyset *keyset_on(rt_ctx *c, uint32_t key_len, uint32_t n_keys, hipStream_t s, Build build) {
+    rt_keyset *k = new rt_keyset();
+    k->ctx = c;
+    k->key_len = key_len;
+    k->n_keys = n_keys;
+    k->nr = key_len == 64 ? 14 : 10;
+    k->home = s;
+    hipError_t e = hipEventCreateWithFlags(&k->ready, hipEventDisableTiming);
+    if (e == hipSuccess) e = rec_alloc(c, (uint64_t)n_keys * REC_WORDS * 4, &k->d_rec, s);
+    if (e != hipSuccess) {
+        fail(RT_E_NOMEM, std::string("key table allocation failed: ") + hipGetErrorString(e));
+        if (k->ready) hipEventDestroy(k->ready);
+        delete k;
+        return nullptr;
+    }
+    if ((e = build(k)) != hipSuccess || (e = hipEventRecord(k->ready, s)) != hipSuccess) {
+        hip_fail(e, "key setup launch");
+        hipStreamSynchronize(s);
+        hipFreeAsync(k->d_rec, s);
+        hipEventDestroy(k->ready);
+        delete k;
+        return nullptr;
+    }
+    return k;
+}
+
 extern "C" {
 
 int rt_abi_version(void) { return RNSTOK_ABI_VERSION; }
@@ -175,13 +249,37 @@ rt_ctx *rt_create(int device) {
     c->n_cu = prop.multiProcessorCount;
     uint8_t tables[512];
     make_sbox(tables, tables + 256);
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->d_sbox, 512) != hipSuccess ||
-        hipMalloc(&c->d_queues, 64ull * rt_ctx::QUEUE_SLOTS) != hipSuccess ||
-        hipMemcpy(c->d_sbox, tables, 512, hipMemcpyHostToDevice) != hipSuccess) {
+    bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipMalloc(&c->d_sbox, 512) == hipSuccess &&
+              hipMalloc(&c->queues.d, 64ull * QueueRing::SLOTS) == hipSuccess &&
+              hipMemcpy(c->d_sbox, tables, 512, hipMemcpyHostToDevice) == hipSuccess;
+    for (uint32_t i = 0; ok && i < QueueRing::SLOTS; ++i)
+        ok = hipEventCreateWithFlags(&c->queues.ev[i], hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; ok && i < N_STAGERS; ++i)
+        ok = hipStreamCreateWithFlags(&c->stagers[i].stream, hipStreamNonBlocking) == hipSuccess;
+    if (!ok) {
         fail(RT_E_HIP, "context setup failed");
         rt_destroy(c);
         return nullptr;
+    }
+    // Key-record pool: keep freed memory for the next key set (no release
+    // on synchronisation), reuse across streams through the stream-ordered
+    // dependencies.  Without a pool the records come from the device's
+    // default one.
+    hipMemPoolProps props = {};
+    props.allocType = hipMemAllocationTypePinned;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = device;
+    if (hipMemPoolCreate(&c->pool, &props) == hipSuccess) {
+        uint64_t keep = ~0ull;
+        int on = 1;
+        hipMemPoolSetAttribute(c->pool, hipMemPoolAttrReleaseThreshold, &keep);
+        hipMemPoolSetAttribute(c->pool, hipMemPoolReuseFollowEventDependencies, &on);
+        hipMemPoolSetAttribute(c->pool, hipMemPoolReuseAllowOpportunistic, &on);
+        hipMemPoolSetAttribute(c->pool, hipMemPoolReuseAllowInternalDependencies, &on);
+    } else {
+        c->pool = nullptr;
+        (void)hipGetLastError();
     }
     return c;
 }
@@ -189,12 +287,19 @@ rt_ctx *rt_create(int device) {
 void rt_destroy(rt_ctx *c) {
     if (!c) return;
     hipSetDevice(c->device);
+    for (auto &g : c->stagers) {
+        if (g.stream) hipStreamSynchronize(g.stream);
+        hipFree(g.d_work);
+        if (g.h_stage) hipHostFree(g.h_stage);
+        if (g.stream) hipStreamDestroy(g.stream);
+    }
     if (c->stream) hipStreamSynchronize(c->stream);
+    hipDeviceSynchronize();            // launches on callers' streams may still use the ring
     hipFree(c->d_sbox);
-    hipFree(c->d_queues);
-    for (auto &e : c->rec_cache) hipFree(e.second);
-    hipFree(c->d_work);
-    if (c->h_stage) hipHostFree(c->h_stage);
+    hipFree(c->queues.d);
+    for (auto &e : c->queues.ev)
+        if (e) hipEventDestroy(e);
+    if (c->pool) hipMemPoolDestroy(c->pool);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -214,53 +319,67 @@ rt_keyset *rt_keyset_create_device(rt_ctx *c, const uint8_t *d_keys, uint32_t ke
         return nullptr;
     }
     hipSetDevice(c->device);
-    rt_keyset *k = new rt_keyset();
-    k->ctx = c;
-    k->key_len = key_len;
-    k->n_keys = n_keys;
-    k->nr = key_len == 64 ? 14 : 10;
     hipStream_t s = pick(c, stream);
-    if (!(k->d_rec = rec_alloc(c, (uint64_t)n_keys * REC_WORDS * 4, &k->rec_cap))) {
-        fail(RT_E_NOMEM, "key table allocation failed");
-        delete k;
-        return nullptr;
-    }
-    hipError_t e = launch_key_setup(d_keys, key_len, n_keys, c->d_sbox, k->d_rec, s);
-    if (e != hipSuccess) {
-        hip_fail(e, "key setup launch");
-        rt_keyset_destroy(k);
-        return nullptr;
-    }
-    return k;
+    return keyset_on(c, key_len, n_keys, s, [&](rt_keyset *k) {
+        return launch_key_setup(d_keys, key_len, n_keys, c->d_sbox, k->d_rec, s);
+    });
 }
 
+// Host keys: staged through a pinned buffer and a staging lane's workspace;
+// the key set is built on that lane's stream and this call does not block
+// (later launches on other streams wait on the key set's ready event).
 rt_keyset *rt_keyset_create(rt_ctx *c, const uint8_t *keys, uint32_t key_len, uint32_t n_keys) {
     if (!c || !keys || n_keys == 0) {
         fail(RT_E_INVAL, "rt_keyset_create: null context/keys or zero keys");
         return nullptr;
     }
-    hipSetDevice(c->device);
-    uint8_t *d_keys = nullptr;
-    const uint64_t bytes = (uint64_t)n_keys * key_len;
-    if (hipMalloc(&d_keys, bytes ? bytes : 1) != hipSuccess) {
-        fail(RT_E_NOMEM, "key upload allocation failed");
+    if (key_len != 64 && key_len != 32) {   // Token.py:72
+        fail(RT_E_INVAL, "Token key must be 128 or 256 bits, not " + std::to_string(key_len * 8));
         return nullptr;
     }
-    rt_keyset *k = nullptr;
-    if (hipMemcpyAsync(d_keys, keys, bytes, hipMemcpyHostToDevice, c->stream) == hipSuccess)
-        k = rt_keyset_create_device(c, d_keys, key_len, n_keys, c->stream);
-    else
-        fail(RT_E_HIP, "key upload failed");
-    hipStreamSynchronize(c->stream);   // the raw keys are not kept on the device
-    hipFree(d_keys);
+    hipSetDevice(c->device);
+    const uint64_t bytes = (uint64_t)n_keys * key_len;
+    StageLock L(c);
+    Stager &g = *L.g;
+    if (ensure_work(g, bytes)) return nullptr;
+    uint8_t *h = stage(g, bytes);
+    hipError_t e;
+    if (h) {
+        memcpy(h, keys, bytes);
+        g.stage_busy = true;
+        e = hipMemcpyAsync(g.d_work, h, bytes, hipMemcpyHostToDevice, g.stream);
+    } else {
+        e = hipMemcpyAsync(g.d_work, keys, bytes, hipMemcpyHostToDevice, g.stream);
+    }
+    if (e != hipSuccess) {
+        hip_fail(e, "key upload failed");
+        return nullptr;
+    }
+    rt_keyset *k = keyset_on(c, key_len, n_keys, g.stream, [&](rt_keyset *ks) {
+        return launch_key_setup(g.d_work, key_len, n_keys, c->d_sbox, ks->d_rec, g.stream);
+    });
+    if (!h) hipStreamSynchronize(g.stream);   // the caller's pageable keys were read in place
     return k;
 }
 
+// No synchronisation: the records go back to the pool on the reclaim stream
+// once the key setup and the last launch on every stream that used them are
+// done.
 void rt_keyset_destroy(rt_keyset *k) {
     if (!k) return;
-    hipSetDevice(k->ctx->device);
-    hipDeviceSynchronize();
-    rec_release(k->ctx, k->d_rec, k->rec_cap);
+    rt_ctx *c = k->ctx;
+    hipSetDevice(c->device);
+    hipStreamWaitEvent(c->stream, k->ready, 0);
+    {
+        std::lock_guard<std::mutex> g(k->mu);
+        for (auto &u : k->uses) {
+            hipStreamWaitEvent(c->stream, u.second, 0);
+            hipEventDestroy(u.second);
+        }
+        k->uses.clear();
+    }
+    hipFreeAsync(k->d_rec, c->stream);
+    hipEventDestroy(k->ready);
     delete k;
 }
 
@@ -278,8 +397,11 @@ static int enc_common(const rt_keyset *k, EncArgs &a, void *stream) {
     if (!a.pt || !a.iv || !a.tok) return fail(RT_E_INVAL, "rt_encrypt: null buffer");
     a.rec = k->d_rec;
     a.sbox = k->ctx->d_sbox;
+    hipStream_t s = pick(k->ctx, stream);
     RT_HIP(hipSetDevice(k->ctx->device), "hipSetDevice");
-    RT_HIP(launch_encrypt(a, k->nr, k->ctx->n_cu, next_queue(k->ctx), pick(k->ctx, stream)), "encrypt launch");
+    RT_HIP(after_setup(k, s), "wait for key setup");
+    RT_HIP(launch_encrypt(a, k->nr, k->ctx->n_cu, &k->ctx->queues, s), "encrypt launch");
+    RT_HIP(note_use(const_cast<rt_keyset *>(k), s), "record key set use");
     return RT_OK;
 }
 
@@ -290,8 +412,11 @@ static int dec_common(const rt_keyset *k, DecArgs &a, void *stream) {
     if (!a.tok || !a.pt || !a.out_len || !a.status) return fail(RT_E_INVAL, "rt_decrypt: null buffer");
     a.rec = k->d_rec;
     a.sbox = k->ctx->d_sbox;
+    hipStream_t s = pick(k->ctx, stream);
     RT_HIP(hipSetDevice(k->ctx->device), "hipSetDevice");
-    RT_HIP(launch_decrypt(a, k->nr, k->ctx->n_cu, next_queue(k->ctx), pick(k->ctx, stream)), "decrypt launch");
+    RT_HIP(after_setup(k, s), "wait for key setup");
+    RT_HIP(launch_decrypt(a, k->nr, k->ctx->n_cu, &k->ctx->queues, s), "decrypt launch");
+    RT_HIP(note_use(const_cast<rt_keyset *>(k), s), "record key set use");
     return RT_OK;
 }
 
@@ -379,15 +504,18 @@ int rt_decrypt_ex(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_of
 
 // ---------------------------------------------------------------- host path
 
-static int ensure_work(rt_ctx *c, uint64_t bytes) {
-    if (bytes <= c->work_cap) return RT_OK;
-    uint64_t cap = std::max<uint64_t>(bytes, c->work_cap * 2);
+static int ensure_work(Stager &g, uint64_t bytes) {
+    if (bytes <= g.work_cap) return RT_OK;
+    uint64_t cap = std::max<uint64_t>(bytes, g.work_cap * 2);
     cap = (cap + 4095) & ~4095ull;
-    hipFree(c->d_work);
-    c->d_work = nullptr;
-    c->work_cap = 0;
-    if (hipMalloc(&c->d_work, cap) != hipSuccess) return fail(RT_E_NOMEM, "workspace allocation failed");
-    c->work_cap = cap;
+    if (g.d_work) {
+        RT_HIP(hipStreamSynchronize(g.stream), "stream sync");   // queued work may still read the old workspace
+        hipFree(g.d_work);
+    }
+    g.d_work = nullptr;
+    g.work_cap = 0;
+    if (hipMalloc(&g.d_work, cap) != hipSuccess) return fail(RT_E_NOMEM, "workspace allocation failed");
+    g.work_cap = cap;
     return RT_OK;
 }
 
@@ -395,27 +523,27 @@ static uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
 
 static constexpr uint64_t STAGE_MAX = 8ull << 20;
 
-// The pinned stage for a token host call of `bytes`, or null (too large, or
-// the pinned allocation failed): the caller then copies from its own pageable
-// arrays.  Called under c->mu.
-static uint8_t *stage(rt_ctx *c, uint64_t bytes) {
+// The pinned stage for a host call of `bytes`, or null (too large, or the
+// pinned allocation failed): the caller then copies from its own pageable
+// arrays.  Called with the lane locked.
+static uint8_t *stage(Stager &g, uint64_t bytes) {
     if (bytes > STAGE_MAX) return nullptr;
-    if (c->stage_busy) {           // an earlier call failed between its copy and its sync
-        if (hipStreamSynchronize(c->stream) != hipSuccess) return nullptr;
-        c->stage_busy = false;
+    if (g.stage_busy) {            // a copy from h_stage may still be queued
+        if (hipStreamSynchronize(g.stream) != hipSuccess) return nullptr;
+        g.stage_busy = false;
     }
-    if (bytes > c->stage_cap) {
-        const uint64_t cap = std::min<uint64_t>(STAGE_MAX, std::max<uint64_t>({bytes, 2 * c->stage_cap, 64ull << 10}));
-        if (c->h_stage) hipHostFree(c->h_stage);
-        c->h_stage = nullptr;
-        c->stage_cap = 0;
-        if (hipHostMalloc(&c->h_stage, cap, hipHostMallocDefault) != hipSuccess) {
-            c->h_stage = nullptr;
+    if (bytes > g.stage_cap) {
+        const uint64_t cap = std::min<uint64_t>(STAGE_MAX, std::max<uint64_t>({bytes, 2 * g.stage_cap, 64ull << 10}));
+        if (g.h_stage) hipHostFree(g.h_stage);
+        g.h_stage = nullptr;
+        g.stage_cap = 0;
+        if (hipHostMalloc(&g.h_stage, cap, hipHostMallocDefault) != hipSuccess) {
+            g.h_stage = nullptr;
             return nullptr;
         }
-        c->stage_cap = cap;
+        g.stage_cap = cap;
     }
-    return c->h_stage;
+    return g.h_stage;
 }
 
 // ----------------------------------------------------------- ratchet trials
@@ -431,8 +559,11 @@ int rt_verify_trials(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok
     TrialArgs a{};
     a.rec = k->d_rec; a.tok = tok; a.tok_off = tok_off; a.tok_len = tok_len; a.pair_off = pair_off;
     a.pair_key = pair_key; a.first = first; a.n_tok = n_tok; a.n_pairs = n_pairs;
+    hipStream_t s = pick(k->ctx, stream);
     RT_HIP(hipSetDevice(k->ctx->device), "hipSetDevice");
-    RT_HIP(launch_verify_trials(a, pick(k->ctx, stream)), "verify trials launch");
+    RT_HIP(after_setup(k, s), "wait for key setup");
+    RT_HIP(launch_verify_trials(a, s), "verify trials launch");
+    RT_HIP(note_use(const_cast<rt_keyset *>(k), s), "record key set use");
     return RT_OK;
 }
 
@@ -455,14 +586,15 @@ int rt_verify_trials_host(const rt_keyset *k, const uint8_t *tok, const uint64_t
         if (pair_key[j] >= k->n_keys) return fail(RT_E_INVAL, "pair_key out of range");
     if (tok_ext && !tok) return fail(RT_E_INVAL, "rt_verify_trials_host: null tokens");
     rt_ctx *c = k->ctx;
-    std::lock_guard<std::mutex> g(c->mu);
+    StageLock L(c);
+    Stager &g = *L.g;
     RT_HIP(hipSetDevice(c->device), "hipSetDevice");
     const uint64_t o_tok = 0, o_to = align16(o_tok + std::max<uint64_t>(tok_ext, 1)), o_tl = align16(o_to + 8ull * n_tok),
                    o_po = align16(o_tl + 4ull * n_tok), o_pk = align16(o_po + 4ull * (n_tok + 1)),
                    o_fi = align16(o_pk + 4ull * std::max<uint32_t>(n_pairs, 1)), total = align16(o_fi + 4ull * n_tok);
-    if ((rc = ensure_work(c, total))) return rc;
-    uint8_t *w = c->d_work;
-    hipStream_t s = c->stream;
+    if ((rc = ensure_work(g, total))) return rc;
+    uint8_t *w = g.d_work;
+    hipStream_t s = g.stream;
     if (tok_ext) RT_HIP(hipMemcpyAsync(w + o_tok, tok, tok_ext, hipMemcpyHostToDevice, s), "H2D tok");
     RT_HIP(hipMemcpyAsync(w + o_to, tok_off, 8ull * n_tok, hipMemcpyHostToDevice, s), "H2D tok_off");
     RT_HIP(hipMemcpyAsync(w + o_tl, tok_len, 4ull * n_tok, hipMemcpyHostToDevice, s), "H2D tok_len");
@@ -493,17 +625,18 @@ int rt_encrypt_host(const rt_keyset *k, const uint8_t *pt, const uint64_t *pt_of
     }
     if (pt_ext && !pt) return fail(RT_E_INVAL, "rt_encrypt_host: null plaintext");
     rt_ctx *c = k->ctx;
-    std::lock_guard<std::mutex> g(c->mu);
+    StageLock L(c);
+    Stager &g = *L.g;
     RT_HIP(hipSetDevice(c->device), "hipSetDevice");
     // inputs first, the token region last: one copy in, one copy out
     const uint64_t o_pt = 0, o_iv = align16(o_pt + std::max<uint64_t>(pt_ext, 1)), o_po = align16(o_iv + 16ull * n),
                    o_pl = align16(o_po + 8ull * n), o_to = align16(o_pl + 4ull * n), o_ki = align16(o_to + 8ull * n),
                    o_tok = align16(o_ki + (key_idx ? 4ull * n : 0)), total = align16(o_tok + tok_ext);
-    if ((rc = ensure_work(c, total))) return rc;
-    uint8_t *w = c->d_work;
-    hipStream_t s = c->stream;
+    if ((rc = ensure_work(g, total))) return rc;
+    uint8_t *w = g.d_work;
+    hipStream_t s = g.stream;
     const bool gaps = tok_sum != tok_ext;   // gaps between tokens: keep the caller's bytes there
-    uint8_t *h = stage(c, total);
+    uint8_t *h = stage(g, total);
     if (h) {
         if (pt_ext) memcpy(h + o_pt, pt, pt_ext);
         memcpy(h + o_iv, iv, 16ull * n);
@@ -512,7 +645,7 @@ int rt_encrypt_host(const rt_keyset *k, const uint8_t *pt, const uint64_t *pt_of
         memcpy(h + o_to, tok_off, 8ull * n);
         if (key_idx) memcpy(h + o_ki, key_idx, 4ull * n);
         if (gaps) memcpy(h + o_tok, tok, tok_ext);
-        c->stage_busy = true;
+        g.stage_busy = true;
         RT_HIP(hipMemcpyAsync(w, h, gaps ? total : o_tok, hipMemcpyHostToDevice, s), "H2D stage");
     } else {
         if (pt_ext) RT_HIP(hipMemcpyAsync(w + o_pt, pt, pt_ext, hipMemcpyHostToDevice, s), "H2D pt");
@@ -530,7 +663,7 @@ int rt_encrypt_host(const rt_keyset *k, const uint8_t *pt, const uint64_t *pt_of
     if ((rc = enc_common(k, a, s))) return rc;
     RT_HIP(hipMemcpyAsync(h ? h + o_tok : tok, w + o_tok, tok_ext, hipMemcpyDeviceToHost, s), "D2H tok");
     RT_HIP(hipStreamSynchronize(s), "stream sync");
-    c->stage_busy = false;
+    g.stage_busy = false;
     if (h) memcpy(tok, h + o_tok, tok_ext);
     return RT_OK;
 }
@@ -552,7 +685,8 @@ int rt_decrypt_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_
     }
     if ((tok_ext && !tok) || (pt_ext && !pt)) return fail(RT_E_INVAL, "rt_decrypt_host: null buffer");
     rt_ctx *c = k->ctx;
-    std::lock_guard<std::mutex> g(c->mu);
+    StageLock L(c);
+    Stager &g = *L.g;
     RT_HIP(hipSetDevice(c->device), "hipSetDevice");
     // inputs first, the outputs (plaintexts, lengths, status) last: one copy
     // in, one copy out
@@ -560,11 +694,11 @@ int rt_decrypt_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_
                    o_po = align16(o_tl + 4ull * n), o_ki = align16(o_po + 8ull * n),
                    o_pt = align16(o_ki + (key_idx ? 4ull * n : 0)), o_ol = align16(o_pt + std::max<uint64_t>(pt_ext, 1)),
                    o_st = align16(o_ol + 4ull * n), total = align16(o_st + 4ull * n);
-    if ((rc = ensure_work(c, total))) return rc;
-    uint8_t *w = c->d_work;
-    hipStream_t s = c->stream;
+    if ((rc = ensure_work(g, total))) return rc;
+    uint8_t *w = g.d_work;
+    hipStream_t s = g.stream;
     const bool gaps = pt_ext && pt_sum != pt_ext;   // gaps between plaintexts: keep the caller's bytes there
-    uint8_t *h = stage(c, total);
+    uint8_t *h = stage(g, total);
     if (h) {
         if (tok_ext) memcpy(h + o_tok, tok, tok_ext);
         memcpy(h + o_to, tok_off, 8ull * n);
@@ -572,7 +706,7 @@ int rt_decrypt_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_
         memcpy(h + o_po, pt_off, 8ull * n);
         if (key_idx) memcpy(h + o_ki, key_idx, 4ull * n);
         if (gaps) memcpy(h + o_pt, pt, pt_ext);
-        c->stage_busy = true;
+        g.stage_busy = true;
         RT_HIP(hipMemcpyAsync(w, h, gaps ? o_ol : o_pt, hipMemcpyHostToDevice, s), "H2D stage");
     } else {
         if (tok_ext) RT_HIP(hipMemcpyAsync(w + o_tok, tok, tok_ext, hipMemcpyHostToDevice, s), "H2D tok");
@@ -591,7 +725,7 @@ int rt_decrypt_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_
     if (h) {
         RT_HIP(hipMemcpyAsync(h + o_pt, w + o_pt, total - o_pt, hipMemcpyDeviceToHost, s), "D2H stage");
         RT_HIP(hipStreamSynchronize(s), "stream sync");
-        c->stage_busy = false;
+        g.stage_busy = false;
         if (pt_ext) memcpy(pt, h + o_pt, pt_ext);
         memcpy(pt_len, h + o_ol, 4ull * n);
         memcpy(status, h + o_st, 4ull * n);
@@ -728,12 +862,13 @@ int rt_resource_hashmap_host(rt_ctx *c, const uint8_t *data, uint64_t size, uint
     if (!data || !hashmap || (rh_len && !random_hash)) return fail(RT_E_INVAL, "rt_resource_hashmap_host: null buffer");
     const uint64_t o_data = 0, o_salt = align16(size), o_out = align16(o_salt + rh_len),
                    o_col = align16(o_out + 4 * parts), total = align16(o_col + 4);
-    std::lock_guard<std::mutex> g(c->mu);
+    StageLock L(c);
+    Stager &g = *L.g;
     RT_HIP(hipSetDevice(c->device), "hipSetDevice");
-    int rc = ensure_work(c, total);
+    int rc = ensure_work(g, total);
     if (rc) return rc;
-    uint8_t *w = c->d_work;
-    hipStream_t s = c->stream;
+    uint8_t *w = g.d_work;
+    hipStream_t s = g.stream;
     RT_HIP(hipMemcpyAsync(w + o_data, data, size, hipMemcpyHostToDevice, s), "H2D data");
     if (rh_len) RT_HIP(hipMemcpyAsync(w + o_salt, random_hash, rh_len, hipMemcpyHostToDevice, s), "H2D salt");
     MapArgs m{};
@@ -796,11 +931,12 @@ int rt_hkdf_host(rt_ctx *c, const uint8_t *ikm, uint64_t ikm_stride, uint32_t ik
                    b_out = (uint64_t)n * length;   // salt_stride 0: one shared salt row
     const uint64_t o_ikm = 0, o_salt = align16(o_ikm + b_ikm), o_ctx = align16(o_salt + b_salt),
                    o_out = align16(o_ctx + context_len), total = align16(o_out + b_out);
-    std::lock_guard<std::mutex> g(c->mu);
+    StageLock L(c);
+    Stager &g = *L.g;
     RT_HIP(hipSetDevice(c->device), "hipSetDevice");
-    if ((rc = ensure_work(c, total))) return rc;
-    uint8_t *w = c->d_work;
-    hipStream_t s = c->stream;
+    if ((rc = ensure_work(g, total))) return rc;
+    uint8_t *w = g.d_work;
+    hipStream_t s = g.stream;
     if (b_ikm)
         RT_HIP(hipMemcpy2DAsync(w + o_ikm, ikm_len, ikm, ikm_stride, ikm_len, n, hipMemcpyHostToDevice, s), "H2D ikm");
     if (b_salt)
@@ -831,21 +967,94 @@ rt_keyset *rt_keyset_create_hkdf(rt_ctx *c, const uint8_t *ikm, uint64_t ikm_str
     }
     hipSetDevice(c->device);
     hipStream_t s = pick(c, stream);
-    uint8_t *d_keys = nullptr;
-    if (hipMallocAsync((void **)&d_keys, (uint64_t)n * key_len, s) != hipSuccess) {
-        fail(RT_E_NOMEM, "derived key buffer allocation failed");
-        return nullptr;
-    }
-    const HkdfArgs a = hkdf_args(ikm, ikm_stride, ikm_len, salt, salt_stride, salt_len, context, context_len, d_keys,
+    const HkdfArgs a = hkdf_args(ikm, ikm_stride, ikm_len, salt, salt_stride, salt_len, context, context_len, nullptr,
                                  key_len, key_len, n);
-    rt_keyset *k = nullptr;
-    hipError_t e = launch_hkdf(a, s);
-    if (e == hipSuccess)
-        k = rt_keyset_create_device(c, d_keys, key_len, n, s);
-    else
-        hip_fail(e, "hkdf launch");
-    hipFreeAsync(d_keys, s);     // stream-ordered: freed after the key setup has consumed it
-    return k;
+    return keyset_on(c, key_len, n, s, [&](rt_keyset *k) {
+        // one launch: derive each key in registers and build its record
+        hipError_t e = launch_hkdf_key_setup(a, c->d_sbox, k->d_rec, c->n_cu, s);
+        if (e != hipErrorNotSupported) return e;
+        // other shapes (context, long or unaligned ikm/salt): HKDF into a
+        // stream-ordered temporary, then the key setup
+        uint8_t *d_keys = nullptr;
+        if ((e = hipMallocAsync((void **)&d_keys, (uint64_t)n * key_len, s)) != hipSuccess) return e;
+        HkdfArgs t = a;
+        t.out = d_keys;
+        e = launch_hkdf(t, s);
+        if (e == hipSuccess) e = launch_key_setup(d_keys, key_len, n, c->d_sbox, k->d_rec, s);
+        hipFreeAsync(d_keys, s);     // freed after the key setup has consumed it
+        return e;
+    });
+}
+
+// ------------------------------------------------------------- verify_hmac
+
+static int verify_common(const rt_keyset *k, VerifyArgs &a, void *stream) {
+    int rc = check_keyset(k);
+    if (rc) return rc;
+    if (a.n == 0) return RT_OK;
+    if (!a.status) return fail(RT_E_INVAL, "rt_verify: null status");
+    a.rec = k->d_rec;
+    hipStream_t s = pick(k->ctx, stream);
+    RT_HIP(hipSetDevice(k->ctx->device), "hipSetDevice");
+    RT_HIP(after_setup(k, s), "wait for key setup");
+    RT_HIP(launch_verify(a, s), "verify launch");
+    RT_HIP(note_use(const_cast<rt_keyset *>(k), s), "record key set use");
+    return RT_OK;
+}
+
+int rt_verify(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,
+              const uint32_t *key_idx, int32_t *status, uint32_t n, void *stream) {
+    if (n && (!tok_off || !tok_len)) return fail(RT_E_INVAL, "rt_verify: null offset/length array");
+    VerifyArgs a{};
+    a.tok = tok; a.tok_off = tok_off; a.tok_len = tok_len; a.key_idx = key_idx; a.status = status; a.n = n;
+    return verify_common(k, a, stream);
+}
+
+int rt_verify_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,
+                   const uint32_t *key_idx, int32_t *status, uint32_t n) {
+    int rc = check_keyset(k);
+    if (rc) return rc;
+    if (n == 0) return RT_OK;
+    if (!tok_off || !tok_len || !status) return fail(RT_E_INVAL, "rt_verify_host: null argument");
+    uint64_t tok_ext = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (key_idx && key_idx[i] >= k->n_keys) return fail(RT_E_INVAL, "key_idx out of range");
+        tok_ext = std::max<uint64_t>(tok_ext, tok_off[i] + tok_len[i]);
+    }
+    if (tok_ext && !tok) return fail(RT_E_INVAL, "rt_verify_host: null tokens");
+    rt_ctx *c = k->ctx;
+    StageLock L(c);
+    Stager &g = *L.g;
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    const uint64_t o_tok = 0, o_to = align16(std::max<uint64_t>(tok_ext, 1)), o_tl = align16(o_to + 8ull * n),
+                   o_ki = align16(o_tl + 4ull * n), o_st = align16(o_ki + (key_idx ? 4ull * n : 0)),
+                   total = align16(o_st + 4ull * n);
+    if ((rc = ensure_work(g, total))) return rc;
+    uint8_t *w = g.d_work;
+    hipStream_t s = g.stream;
+    uint8_t *h = stage(g, total);
+    if (h) {
+        if (tok_ext) memcpy(h + o_tok, tok, tok_ext);
+        memcpy(h + o_to, tok_off, 8ull * n);
+        memcpy(h + o_tl, tok_len, 4ull * n);
+        if (key_idx) memcpy(h + o_ki, key_idx, 4ull * n);
+        g.stage_busy = true;
+        RT_HIP(hipMemcpyAsync(w, h, o_st, hipMemcpyHostToDevice, s), "H2D stage");
+    } else {
+        if (tok_ext) RT_HIP(hipMemcpyAsync(w + o_tok, tok, tok_ext, hipMemcpyHostToDevice, s), "H2D tok");
+        RT_HIP(hipMemcpyAsync(w + o_to, tok_off, 8ull * n, hipMemcpyHostToDevice, s), "H2D tok_off");
+        RT_HIP(hipMemcpyAsync(w + o_tl, tok_len, 4ull * n, hipMemcpyHostToDevice, s), "H2D tok_len");
+        if (key_idx) RT_HIP(hipMemcpyAsync(w + o_ki, key_idx, 4ull * n, hipMemcpyHostToDevice, s), "H2D key_idx");
+    }
+    VerifyArgs a{};
+    a.tok = w + o_tok; a.tok_off = (const uint64_t *)(w + o_to); a.tok_len = (const uint32_t *)(w + o_tl);
+    a.key_idx = key_idx ? (const uint32_t *)(w + o_ki) : nullptr; a.status = (int32_t *)(w + o_st); a.n = n;
+    if ((rc = verify_common(k, a, s))) return rc;
+    RT_HIP(hipMemcpyAsync(h ? h + o_st : (uint8_t *)status, w + o_st, 4ull * n, hipMemcpyDeviceToHost, s), "D2H status");
+    RT_HIP(hipStreamSynchronize(s), "stream sync");
+    g.stage_busy = false;
+    if (h) memcpy(status, h + o_st, 4ull * n);
+    return RT_OK;
 }
 
 // ------------------------------------------------------------------ memory

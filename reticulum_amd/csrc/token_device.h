@@ -220,6 +220,23 @@ __device__ __forceinline__ void sha256_compress(uint32_t h[8], const uint32_t w[
     S.finish(h);
 }
 
+// The same with the scheduler fenced every 4 rounds: a message whose words
+// are all known up front otherwise has its whole schedule (W[16..63] + K)
+// hoisted ahead of the rounds, 64 live values; kernels that run many
+// compressions back to back at 3 waves/SIMD (k_hkdf_key_setup) spilled them.
+__device__ __forceinline__ void sha256_compress_fenced(uint32_t h[8], const uint32_t w[16]) {
+    Sha256 S;
+    S.start(h);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) S.w[k] = w[k];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+        S.round(i);
+        if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+    S.finish(h);
+}
+
 // SHA-256 message words from four 16-B units (big-endian words).
 __device__ __forceinline__ void sha_units(uint32_t w[16], u32x4 a, u32x4 b, u32x4 c, u32x4 d) {
     w[0] = bswap(a.x); w[1] = bswap(a.y); w[2] = bswap(a.z); w[3] = bswap(a.w);

@@ -14,6 +14,7 @@
 // Launch shape: one 1024-thread (single key) or 768/512-thread (per-packet keys)
 // workgroup per CU, persistent over the batch; the LDS table image is built
 // once per workgroup.  See DESIGN.md.
+#include "keysetup_device.h"
 #include "token_device.h"
 #include "token_launch.h"
 
@@ -932,6 +933,83 @@ hipError_t launch_verify_trials(const TrialArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------ verify_hmac --
+//
+// Token.verify_hmac (Token.py:77-84): HMAC-SHA256 over token[:-32] under the
+// key's midstates, compared with token[-32:].  One lane per token; any length
+// above 32 B (verify_hmac does not require whole AES blocks): full 64-B blocks
+// from 16-B loads, the last partial block from 16-B units when it is whole
+// units and from byte loads otherwise.  No AES runs and nothing but the status
+// is written.
+
+// rem (< 64) message bytes at p, then 0x80, zeros and the 64-bit length
+// `bits`: the final one or two SHA-256 blocks, from byte loads.
+__device__ __forceinline__ void sha_tail_bytes(uint32_t h[8], const uint8_t *p, uint32_t rem, uint64_t bits) {
+    const uint32_t blocks = rem + 9u <= 64u ? 1u : 2u;
+#pragma nounroll
+    for (uint32_t b = 0; b < blocks; ++b) {
+        uint32_t w[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t q = 64u * b + 4u * k + j;
+                v = (v << 8) | (q < rem ? (uint32_t)p[q] : (q == rem ? 0x80u : 0u));
+            }
+            w[k] = v;
+        }
+        if (b + 1u == blocks) {
+            w[14] = (uint32_t)(bits >> 32);
+            w[15] = (uint32_t)bits;
+        }
+        sha256_compress(h, w);
+    }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_verify(VerifyArgs a) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const uint32_t T = a.tok_len ? a.tok_len[i] : a.uni_len;
+    if (T <= 32u) {                                   // Token.py:78
+        a.status[i] = 1;
+        return;
+    }
+    const uint8_t *Kt = a.tok + (a.tok_off ? a.tok_off[i] : (uint64_t)i * a.tok_stride);
+    const uint32_t *r = a.rec + (a.key_idx ? (uint64_t)a.key_idx[i] * REC_WORDS : 0ull);
+    uint32_t h[8], opad[8], tag[8];
+    load8(h, r + REC_IPAD);
+    const uint32_t M = T - 32u, full = M >> 6, rem = M & 63u;
+    const uint64_t bits = (uint64_t)(64u + M) * 8u;
+    for (uint32_t b = 0; b < full; ++b) {
+        const uint8_t *B = Kt + 64ull * b;
+        uint32_t w[16];
+        sha_units(w, ld16(B), ld16(B + 16), ld16(B + 32), ld16(B + 48));
+        sha256_compress(h, w);
+    }
+    const uint8_t *R = Kt + 64ull * full;
+    if ((rem & 15u) == 0u) {                          // whole 16-B units (every well-formed token)
+        const uint32_t fu = rem >> 4;
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        sha_final_units(h, fu, fu > 0 ? ld16(R) : z, fu > 1 ? ld16(R + 16) : z, fu > 2 ? ld16(R + 32) : z, bits);
+    } else {
+        sha_tail_bytes(h, R, rem, bits);
+    }
+    load8(opad, r + REC_OPAD);
+    hmac_outer(tag, h, opad);
+    const u32x4 r0 = ld16(Kt + M), r1 = ld16(Kt + M + 16);
+    const uint32_t diff = (r0.x ^ bswap(tag[0])) | (r0.y ^ bswap(tag[1])) | (r0.z ^ bswap(tag[2])) |
+                          (r0.w ^ bswap(tag[3])) | (r1.x ^ bswap(tag[4])) | (r1.y ^ bswap(tag[5])) |
+                          (r1.z ^ bswap(tag[6])) | (r1.w ^ bswap(tag[7]));
+    a.status[i] = diff ? 2 : 0;                       // Token.py:82-84
+}
+
+hipError_t launch_verify(const VerifyArgs &a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_verify, dim3((a.n + 255u) / 256u), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------ length bucketing --
 //
 // Three small passes (histogram, scan, scatter) build a permutation that
@@ -1017,187 +1095,32 @@ hipError_t launch_length_order(const uint32_t *len, uint32_t n, int dec, void *w
 
 // ------------------------------------------------------------- key setup --
 
-// Packed GF(2^8) doubling of the four bytes of a word (xtime, aes256.py:86).
-__device__ __forceinline__ uint32_t xt4(uint32_t x) {
-    return ((x & 0x7f7f7f7fu) << 1) ^ (((x >> 7) & 0x01010101u) * 0x1bu);
-}
-// InvMixColumns of one column (aes256.py:101 inv_mix_columns): byte i of the
-// result is 14*a_i ^ 11*a_{i+1} ^ 13*a_{i+2} ^ 9*a_{i+3}.
-__device__ __forceinline__ uint32_t inv_mix_word(uint32_t x) {
-    const uint32_t x2 = xt4(x), x4 = xt4(x2), x8 = xt4(x4);
-    return (x8 ^ x4 ^ x2) ^ rotr(x8 ^ x2 ^ x, 8) ^ rotr(x8 ^ x4 ^ x, 16) ^ rotr(x8 ^ x, 24);
-}
-__device__ __forceinline__ uint32_t sub_word(const uint8_t *sb, uint32_t w) {
-    return (uint32_t)sb[w & 255u] | ((uint32_t)sb[(w >> 8) & 255u] << 8) | ((uint32_t)sb[(w >> 16) & 255u] << 16) |
-           ((uint32_t)sb[w >> 24] << 24);
-}
-
-// One lane per key; NK = 8 (64-byte keys, AES-256) or 4 (32-byte keys, AES-128).
+// One lane per key, records staged through LDS (keysetup_device.h).
+// NK = 8 (64-byte keys, AES-256) or 4 (32-byte keys, AES-128).
 template <int NK>
 __global__ __launch_bounds__(256) void k_key_setup(const uint8_t *keys, uint32_t n_keys, const uint8_t *sbox,
                                                     uint32_t *rec_out) {
     __shared__ uint8_t sb[256];
-    sb[threadIdx.x] = sbox[threadIdx.x];          // blockDim.x == 256
-    __syncthreads();
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_keys) return;
-    constexpr int HALF = 4 * NK, NR = NK + 6, TOTAL = 4 * (NR + 1);
-    const uint8_t *key = keys + (uint64_t)k * (2 * HALF);
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    v4u *rec = (v4u *)(rec_out + (uint64_t)k * REC_WORDS);      // 544-byte records, 16-byte aligned
-    const uint8_t *ek = key + HALF;                              // sk = key[:HALF], ek = key[HALF:]  (Token.py:61-70)
-    uint32_t w[TOTAL];
-#pragma unroll
-    for (int i = 0; i < NK; ++i)
-        w[i] = (uint32_t)ek[4 * i] | ((uint32_t)ek[4 * i + 1] << 8) | ((uint32_t)ek[4 * i + 2] << 16) |
-               ((uint32_t)ek[4 * i + 3] << 24);
-    uint32_t rcon = 1;
-#pragma unroll
-    for (int i = NK; i < TOTAL; ++i) {          // aes256.py:146-175 (aes128.py for NK = 4)
-        uint32_t t = w[i - 1];
-        if (i % NK == 0) {
-            t = sub_word(sb, (t >> 8) | (t << 24)) ^ rcon;      // RotWord, SubWord, Rcon in byte 0
-            rcon = xt4(rcon);
-        } else if (NK > 6 && i % NK == 4) {
-            t = sub_word(sb, t);
-        }
-        w[i] = w[i - NK] ^ t;
-    }
-#pragma unroll
-    for (int q = 0; q < 15; ++q)
-        rec[(REC_ENC >> 2) + q] = 4 * q < TOTAL ? v4u{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]} : v4u{0, 0, 0, 0};
-    // equivalent inverse cipher: dk[0] = rk[nr], dk[r] = InvMix(rk[nr-r]), dk[nr] = rk[0]
-#pragma unroll
-    for (int r = 0; r < 15; ++r) {
-        v4u d = {0, 0, 0, 0};
-        if (r <= NR) {
-            const int o = 4 * (NR - r);
-            d = (r == 0 || r == NR) ? v4u{w[o], w[o + 1], w[o + 2], w[o + 3]}
-                                    : v4u{inv_mix_word(w[o]), inv_mix_word(w[o + 1]), inv_mix_word(w[o + 2]),
-                                          inv_mix_word(w[o + 3])};
-        }
-        rec[(REC_DEC >> 2) + r] = d;
-    }
-    // HMAC midstates (HMAC.py:73-82): sk zero-padded to 64 B, ^0x36 / ^0x5c
-    uint32_t bi[16], bo[16], hi[8], ho[8];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        uint32_t v = 0;
-        if (4 * i < HALF)
-            v = ((uint32_t)key[4 * i] << 24) | ((uint32_t)key[4 * i + 1] << 16) | ((uint32_t)key[4 * i + 2] << 8) |
-                key[4 * i + 3];
-        bi[i] = v ^ 0x36363636u;
-        bo[i] = v ^ 0x5c5c5c5cu;
-    }
-    const uint32_t iv0[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
-                             0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-#pragma unroll
-    for (int i = 0; i < 8; ++i) hi[i] = ho[i] = iv0[i];
-    sha256_compress(hi, bi);
-    sha256_compress(ho, bo);
-    rec[REC_IPAD >> 2] = v4u{hi[0], hi[1], hi[2], hi[3]};
-    rec[(REC_IPAD >> 2) + 1] = v4u{hi[4], hi[5], hi[6], hi[7]};
-    rec[REC_OPAD >> 2] = v4u{ho[0], ho[1], ho[2], ho[3]};
-    rec[(REC_OPAD >> 2) + 1] = v4u{ho[4], ho[5], ho[6], ho[7]};
-}
-
-// The same records, written through LDS.  A lane's record is 34 16-B pieces at
-// a 544-B lane stride, so a direct store instruction touches 64 lines; here
-// each wave stages KS_P pieces of its 64 records per round and stores the
-// wave's records as runs of KS_P * 16 contiguous bytes (≈64 / KS_P runs per store
-// instead of 64 pieces).  Records of consecutive keys are adjacent in HBM.
-#ifndef RNSTOK_KS_P
-#define RNSTOK_KS_P 12
-#endif
-constexpr int KS_P = RNSTOK_KS_P, KS_PIECES = REC_WORDS / 4, KS_ROUNDS = (KS_PIECES + KS_P - 1) / KS_P;
-template <int NK>
-__global__ __launch_bounds__(256) void k_key_setup_staged(const uint8_t *keys, uint32_t n_keys, const uint8_t *sbox,
-                                                           uint32_t *rec_out) {
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    __shared__ uint8_t sb[256];
-    __shared__ v4u stage[4][64 * KS_P];
+    __shared__ u32x4 stage[4][KS_STAGE_PIECES];
     sb[threadIdx.x] = sbox[threadIdx.x];          // blockDim.x == 256
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t kbase = blockIdx.x * blockDim.x + (wave << 6);
     const uint32_t k = kbase + lane < n_keys ? kbase + lane : n_keys - 1;   // tail lanes recompute the last key
-    constexpr int HALF = 4 * NK, NR = NK + 6, TOTAL = 4 * (NR + 1);
+    constexpr int HALF = 4 * NK;
     const uint8_t *key = keys + (uint64_t)k * (2 * HALF);
     const uint8_t *ek = key + HALF;                              // sk = key[:HALF], ek = key[HALF:]  (Token.py:61-70)
-    uint32_t w[TOTAL];
+    uint32_t ekw[NK], skw[16];
 #pragma unroll
     for (int i = 0; i < NK; ++i)
-        w[i] = (uint32_t)ek[4 * i] | ((uint32_t)ek[4 * i + 1] << 8) | ((uint32_t)ek[4 * i + 2] << 16) |
-               ((uint32_t)ek[4 * i + 3] << 24);
-    uint32_t rcon = 1;
+        ekw[i] = (uint32_t)ek[4 * i] | ((uint32_t)ek[4 * i + 1] << 8) | ((uint32_t)ek[4 * i + 2] << 16) |
+                 ((uint32_t)ek[4 * i + 3] << 24);
 #pragma unroll
-    for (int i = NK; i < TOTAL; ++i) {          // aes256.py:146-175 (aes128.py for NK = 4)
-        uint32_t t = w[i - 1];
-        if (i % NK == 0) {
-            t = sub_word(sb, (t >> 8) | (t << 24)) ^ rcon;
-            rcon = xt4(rcon);
-        } else if (NK > 6 && i % NK == 4) {
-            t = sub_word(sb, t);
-        }
-        w[i] = w[i - NK] ^ t;
-    }
-    // HMAC midstates (HMAC.py:73-82): sk zero-padded to 64 B, ^0x36 / ^0x5c
-    uint32_t bi[16], bo[16], hi[8], ho[8];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        uint32_t v = 0;
-        if (4 * i < HALF)
-            v = ((uint32_t)key[4 * i] << 24) | ((uint32_t)key[4 * i + 1] << 16) | ((uint32_t)key[4 * i + 2] << 8) |
-                key[4 * i + 3];
-        bi[i] = v ^ 0x36363636u;
-        bo[i] = v ^ 0x5c5c5c5cu;
-    }
-    const uint32_t iv0[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
-                             0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-#pragma unroll
-    for (int i = 0; i < 8; ++i) hi[i] = ho[i] = iv0[i];
-    sha256_compress(hi, bi);
-    sha256_compress(ho, bo);
-    v4u *st = stage[wave];
-    v4u *out = (v4u *)rec_out;
-    const uint32_t nvalid = kbase < n_keys ? (n_keys - kbase < 64u ? n_keys - kbase : 64u) : 0u;   // records this wave stores
-#pragma unroll
-    for (int r = 0; r < KS_ROUNDS; ++r) {
-#pragma unroll
-        for (int j = 0; j < KS_P; ++j) {
-            const int c = r * KS_P + j;              // piece c of the record: words 4c..4c+3
-            if (c < KS_PIECES) {
-                v4u d = {0, 0, 0, 0};
-                if (c < 15) {                        // REC_ENC: round keys
-                    if (4 * c < TOTAL) d = v4u{w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]};
-                } else if (c < 30) {                 // REC_DEC: dk[0] = rk[nr], dk[q] = InvMix(rk[nr-q]), dk[nr] = rk[0]
-                    const int q = c - 15;
-                    if (q <= NR) {
-                        const int o = 4 * (NR - q);
-                        d = (q == 0 || q == NR) ? v4u{w[o], w[o + 1], w[o + 2], w[o + 3]}
-                                                : v4u{inv_mix_word(w[o]), inv_mix_word(w[o + 1]),
-                                                      inv_mix_word(w[o + 2]), inv_mix_word(w[o + 3])};
-                    }
-                } else if (c == 30) {
-                    d = v4u{hi[0], hi[1], hi[2], hi[3]};
-                } else if (c == 31) {
-                    d = v4u{hi[4], hi[5], hi[6], hi[7]};
-                } else if (c == 32) {
-                    d = v4u{ho[0], ho[1], ho[2], ho[3]};
-                } else {
-                    d = v4u{ho[4], ho[5], ho[6], ho[7]};
-                }
-                st[lane * KS_P + j] = d;
-            }
-        }
-        __syncthreads();
-        const uint32_t NP = (KS_PIECES - r * KS_P) < KS_P ? (KS_PIECES - r * KS_P) : KS_P;   // constant once unrolled
-        for (uint32_t t = lane; t < nvalid * NP; t += 64u) {
-            const uint32_t rr = t / NP, pc = t - rr * NP;
-            out[(uint64_t)(kbase + rr) * KS_PIECES + r * KS_P + pc] = st[rr * KS_P + pc];
-        }
-        __syncthreads();
-    }
+    for (int i = 0; i < 16; ++i)
+        skw[i] = 4 * i < HALF ? ((uint32_t)key[4 * i] << 24) | ((uint32_t)key[4 * i + 1] << 16) |
+                                    ((uint32_t)key[4 * i + 2] << 8) | key[4 * i + 3]
+                              : 0u;
+    key_record<NK>(sb, ekw, skw, stage[wave], lane, kbase, n_keys, rec_out);
 }
 
 // --------------------------------------------------------------- launchers --
@@ -1285,14 +1208,17 @@ static hipError_t launch_enc_long4_nr(const EncArgs &a, int n_cu, hipStream_t s)
 // per lane) would leave a third of the workgroups one packet longer; there
 // the dynamic chunk loop balances the SIMDs instead.
 template <class Args>
-static hipError_t balance(Args &a, Shape sh, uint32_t *spare, hipStream_t s) {
+static hipError_t balance(Args &a, Shape sh, SpareQueue *spare, hipStream_t s, bool *took) {
     const uint64_t lanes = (uint64_t)sh.grid * (uint64_t)sh.threads;
+    *took = false;
     if (a.queue || !spare || a.n <= lanes || a.n % lanes == 0 || a.n > QUEUE_MAX_N) return hipSuccess;
-    a.queue = spare;
-    return hipMemsetAsync(spare, 0, 4, s);
+    a.queue = spare->acquire(s);
+    if (!a.queue) return hipSuccess;     // no slot: the static stride (correct, less balanced)
+    *took = true;
+    return hipMemsetAsync(a.queue, 0, 4, s);
 }
 
-hipError_t launch_encrypt(const EncArgs &args, int nr, int n_cu, uint32_t *spare, hipStream_t s) {
+hipError_t launch_encrypt(const EncArgs &args, int nr, int n_cu, SpareQueue *spare, hipStream_t s) {
     EncArgs a = args;
 #ifndef RNSTOK_NO_LONG4
     if (!a.key_idx && use_long(a.n, a.pt_len, a.uni_len, n_cu))
@@ -1301,9 +1227,11 @@ hipError_t launch_encrypt(const EncArgs &args, int nr, int n_cu, uint32_t *spare
     if (use_long(a.n, a.pt_len, a.uni_len, n_cu))
         return nr == 14 ? launch_enc_long_nr<14>(a, n_cu, s) : launch_enc_long_nr<10>(a, n_cu, s);
     const Shape sh = shape_for(a.n, a.key_idx ? WG_PERKEY_ENC : WG_ENC, n_cu);
-    const hipError_t e = balance(a, sh, spare, s);
-    if (e != hipSuccess) return e;
-    return nr == 14 ? launch_enc_nr<14>(a, sh, s) : launch_enc_nr<10>(a, sh, s);
+    bool took = false;
+    hipError_t e = balance(a, sh, spare, s, &took);
+    if (e == hipSuccess) e = nr == 14 ? launch_enc_nr<14>(a, sh, s) : launch_enc_nr<10>(a, sh, s);
+    if (took) spare->release(s);
+    return e;
 }
 #ifndef RNSTOK_DEC_LONG_WAVES
 #define RNSTOK_DEC_LONG_WAVES 8
@@ -1317,7 +1245,7 @@ static hipError_t launch_dec_long_nr(const DecArgs &a, int n_cu, hipStream_t s) 
     return hipGetLastError();
 }
 
-hipError_t launch_decrypt(const DecArgs &args, int nr, int n_cu, uint32_t *spare, hipStream_t s) {
+hipError_t launch_decrypt(const DecArgs &args, int nr, int n_cu, SpareQueue *spare, hipStream_t s) {
     DecArgs a = args;
     // long mode: one key, uniform well-formed tokens of >= 1 KiB body, few per CU
     if (!a.key_idx && a.tok_len == nullptr && a.uni_len >= 48u + 1024u && ((a.uni_len - 48u) & 15u) == 0 &&
@@ -1327,23 +1255,18 @@ hipError_t launch_decrypt(const DecArgs &args, int nr, int n_cu, uint32_t *spare
     const uint64_t per_cu = ((uint64_t)a.n + n_cu - 1) / n_cu;
     const int max_t = a.key_idx ? WG_PERKEY_DEC : (per_cu <= 1024u ? 1024 : WG_DEC);
     const Shape sh = shape_for(a.n, max_t, n_cu);
-    const hipError_t e = balance(a, sh, spare, s);
-    if (e != hipSuccess) return e;
-    return nr == 14 ? launch_dec_nr<14>(a, sh, s) : launch_dec_nr<10>(a, sh, s);
+    bool took = false;
+    hipError_t e = balance(a, sh, spare, s, &took);
+    if (e == hipSuccess) e = nr == 14 ? launch_dec_nr<14>(a, sh, s) : launch_dec_nr<10>(a, sh, s);
+    if (took) spare->release(s);
+    return e;
 }
 hipError_t launch_key_setup(const uint8_t *keys, uint32_t key_len, uint32_t n_keys, const uint8_t *sbox,
                             uint32_t *rec, hipStream_t s) {
-#ifndef RNSTOK_KS_DIRECT
-    if (key_len == 64)
-        hipLaunchKernelGGL(k_key_setup_staged<8>, dim3((n_keys + 255) / 256), dim3(256), 0, s, keys, n_keys, sbox, rec);
-    else
-        hipLaunchKernelGGL(k_key_setup_staged<4>, dim3((n_keys + 255) / 256), dim3(256), 0, s, keys, n_keys, sbox, rec);
-#else
     if (key_len == 64)
         hipLaunchKernelGGL(k_key_setup<8>, dim3((n_keys + 255) / 256), dim3(256), 0, s, keys, n_keys, sbox, rec);
     else
         hipLaunchKernelGGL(k_key_setup<4>, dim3((n_keys + 255) / 256), dim3(256), 0, s, keys, n_keys, sbox, rec);
-#endif
     return hipGetLastError();
 }
 hipError_t configure_kernels() {

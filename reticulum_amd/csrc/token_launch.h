@@ -139,13 +139,41 @@ constexpr uint32_t SORT_BUCKETS = 4096;
 uint64_t sort_workspace_bytes(uint32_t n);    // order[n] + 2 x SORT_BUCKETS counters
 hipError_t launch_length_order(const uint32_t *len, uint32_t n, int dec, void *workspace, const uint32_t **order,
                                uint32_t **queue, int n_cu, hipStream_t s);
-// spare_queue: a counter slot the launch may zero and use as a.queue when the
-// static stride would leave a ragged last pass (null: never).
-hipError_t launch_encrypt(const EncArgs &a, int nr, int n_cu, uint32_t *spare_queue, hipStream_t s);
-hipError_t launch_decrypt(const DecArgs &a, int nr, int n_cu, uint32_t *spare_queue, hipStream_t s);
+// Chunk counters for ragged uniform batches (the static stride would leave a
+// ragged last pass).  acquire() hands out a 4-byte device counter that no
+// other launch can still be reading once work queued on `s` after this call
+// runs (the C-ABI orders slot reuse with an event per slot); release() is
+// called once after the launch that used it has been enqueued on `s`.
+struct SpareQueue {
+    virtual uint32_t *acquire(hipStream_t s) = 0;
+    virtual void release(hipStream_t s) = 0;
+    virtual ~SpareQueue() {}
+};
+hipError_t launch_encrypt(const EncArgs &a, int nr, int n_cu, SpareQueue *spare, hipStream_t s);
+hipError_t launch_decrypt(const DecArgs &a, int nr, int n_cu, SpareQueue *spare, hipStream_t s);
+// Token.verify_hmac (Token.py:77-84) over n tokens: status[i] = 0 (tag
+// valid), 1 (len <= 32) or 2 (tag mismatch); no AES, no plaintext.
+struct VerifyArgs {
+    const uint32_t *rec;
+    const uint8_t *tok;
+    const uint64_t *tok_off;    // null -> i * tok_stride
+    uint64_t tok_stride;
+    const uint32_t *tok_len;    // null -> uni_len
+    uint32_t uni_len;
+    const uint32_t *key_idx;    // null -> key 0
+    int32_t *status;
+    uint32_t n;
+};
+hipError_t launch_verify(const VerifyArgs &a, hipStream_t s);
 hipError_t launch_map_hashes(const MapArgs &m, hipStream_t s);
 hipError_t launch_hkdf(const HkdfArgs &a, hipStream_t s);
 hipError_t launch_key_setup(const uint8_t *keys, uint32_t key_len, uint32_t n_keys, const uint8_t *sbox,
                             uint32_t *rec, hipStream_t s);
+// HKDF (a.length = key_len, a.out unused) and key setup in one launch: key i
+// of the records is Token(hkdf(key_len, ikm_i, salt_i, context)) and the
+// derived key never reaches HBM.  Returns hipErrorNotSupported for shapes
+// outside the fused kernel's (the caller then runs launch_hkdf +
+// launch_key_setup through a temporary).
+hipError_t launch_hkdf_key_setup(const HkdfArgs &a, const uint8_t *sbox, uint32_t *rec, int n_cu, hipStream_t s);
 
 }  // namespace rnstok

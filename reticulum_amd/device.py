@@ -8,7 +8,7 @@ synchronised.  torch is used only for device memory and streams.
 import torch
 
 from . import _native
-from .token import KeySet
+from .token import KeySet, token_len
 
 
 def _p(t):
@@ -54,31 +54,74 @@ def _check_u8(*ts):
             raise ValueError("byte buffers must be torch.uint8")
 
 
+def _check_i32(n, **ts):
+    """(n,) contiguous int32 device tensors (None allowed): lengths, statuses
+    and key indices are read and written as 32-bit words by the kernels."""
+    for name, t in ts.items():
+        if t is None:
+            continue
+        if t.dtype != torch.int32 or t.numel() != n or not t.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous ({n},) int32 tensor")
+
+
+def _check_i64(n, **ts):
+    for name, t in ts.items():
+        if t is not None and (t.dtype != torch.int64 or t.numel() != n or not t.is_contiguous()):
+            raise ValueError(f"{name} must be a contiguous ({n},) int64 tensor")
+
+
+def _check_rows(name, t, n, width):
+    """An (n, row) uint8 matrix whose rows hold at least `width` bytes."""
+    if t.dim() != 2 or t.shape[0] != n:
+        raise ValueError(f"{name} must be an ({n}, row) uint8 matrix")
+    if t.shape[1] < width:
+        raise ValueError(f"{name} rows hold {t.shape[1]} bytes, need {width}")
+
+
+def _check_iv(iv, n):
+    if iv.numel() < 16 * n or (iv.dim() == 2 and iv.shape[1] != 16) or not iv.is_contiguous():
+        raise ValueError(f"iv must be a contiguous ({n}, 16) uint8 tensor")
+
+
 def encrypt_uniform(ks: KeySet, pt, pt_len, iv, tok, key_idx=None, stream=None):
     """pt: (n, >= pt_len) uint8 rows; iv: (n, 16) uint8; tok: (n, >=
     token_len(pt_len)) uint8 rows; key_idx: (n,) int32 or None.  pt and tok
     may be row views of wider buffers (their row stride is used)."""
     _check_u8(pt, iv, tok)
     n = pt.shape[0]
-    if iv.numel() < 16 * n or tok.shape[0] != n:
-        raise ValueError("shape mismatch")
-    if key_idx is not None and (key_idx.numel() != n or key_idx.dtype != torch.int32):
-        raise ValueError("key_idx must be (n,) int32")
+    _check_rows("pt", pt, n, pt_len)
+    _check_rows("tok", tok, n, token_len(pt_len))
+    _check_iv(iv, n)
+    _check_i32(n, key_idx=key_idx)
     lib = _native.load()
     _native.check(lib.rt_encrypt_uniform(ks.handle, _p_rows(pt), pt.stride(0), pt_len, _p(key_idx), _p(iv),
                                          _p_rows(tok), tok.stride(0), n, _stream(stream)))
 
 
 def decrypt_uniform(ks: KeySet, tok, tok_len, pt, out_len, status, key_idx=None, stream=None):
-    """tok: (n, tok_stride) uint8 holding tok_len-byte tokens; pt: (n, pt_stride)
-    uint8 with pt_stride >= tok_len - 48; out_len/status: (n,) int32."""
+    """tok: (n, >= tok_len) uint8 holding tok_len-byte tokens; pt: (n, >=
+    tok_len - 48) uint8; out_len/status/key_idx: (n,) int32."""
     _check_u8(tok, pt)
     n = tok.shape[0]
-    if pt.shape[0] != n or out_len.numel() != n or status.numel() != n:
-        raise ValueError("shape mismatch")
+    _check_rows("tok", tok, n, tok_len)
+    _check_rows("pt", pt, n, max(tok_len - 48, 0))
+    _check_i32(n, out_len=out_len, status=status, key_idx=key_idx)
     lib = _native.load()
     _native.check(lib.rt_decrypt_uniform(ks.handle, _p_rows(tok), tok.stride(0), tok_len, _p(key_idx), _p_rows(pt),
                                          pt.stride(0), _p(out_len), _p(status), n, _stream(stream)))
+
+
+def verify(ks: KeySet, tok, tok_off, tok_len, status, key_idx=None, stream=None):
+    """Token.verify_hmac (Token.py:77-84) over device buffers, no AES: token
+    i is tok[tok_off[i] : +tok_len[i]] (int64 / int32); status (n,) int32
+    receives RT_ST_OK (tag valid), RT_ST_BAD_HMAC or RT_ST_TOO_SHORT."""
+    _check_u8(tok)
+    n = tok_off.numel()
+    _check_i64(n, tok_off=tok_off)
+    _check_i32(n, tok_len=tok_len, status=status, key_idx=key_idx)
+    lib = _native.load()
+    _native.check(lib.rt_verify(ks.handle, _p(tok), _p(tok_off), _p(tok_len), _p(key_idx), _p(status), n,
+                                _stream(stream)))
 
 
 def verify_trials(ks: KeySet, tok, tok_off, tok_len, pair_off, pair_key, first, stream=None):
@@ -89,8 +132,10 @@ def verify_trials(ks: KeySet, tok, tok_off, tok_len, pair_off, pair_key, first, 
     opens token t, or -1."""
     _check_u8(tok)
     n = tok_off.numel()
-    if tok_len.numel() != n or pair_off.numel() != n + 1 or first.numel() != n:
-        raise ValueError("shape mismatch")
+    _check_i64(n, tok_off=tok_off)
+    _check_i32(n, tok_len=tok_len, first=first)
+    _check_i32(n + 1, pair_off=pair_off)
+    _check_i32(pair_key.numel(), pair_key=pair_key)
     lib = _native.load()
     _native.check(lib.rt_verify_trials(ks.handle, _p(tok), _p(tok_off), _p(tok_len), _p(pair_off), _p(pair_key),
                                        _p(first), n, pair_key.numel(), _stream(stream)))
@@ -108,6 +153,9 @@ def encrypt(ks: KeySet, pt, pt_off, pt_len, iv, tok, tok_off, key_idx=None, stre
     the device first (same outputs; wavefronts carry similar lengths)."""
     _check_u8(pt, iv, tok)
     n = pt_off.numel()
+    _check_i64(n, pt_off=pt_off, tok_off=tok_off)
+    _check_i32(n, pt_len=pt_len, key_idx=key_idx)
+    _check_iv(iv, n)
     lib = _native.load()
     if sort:
         ws = workspace if workspace is not None else _workspace(n, pt.device)
@@ -122,6 +170,8 @@ def decrypt(ks: KeySet, tok, tok_off, tok_len, pt, pt_off, out_len, status, key_
             workspace=None):
     _check_u8(tok, pt)
     n = tok_off.numel()
+    _check_i64(n, tok_off=tok_off, pt_off=pt_off)
+    _check_i32(n, tok_len=tok_len, out_len=out_len, status=status, key_idx=key_idx)
     lib = _native.load()
     if sort:
         ws = workspace if workspace is not None else _workspace(n, tok.device)
@@ -156,7 +206,9 @@ def hkdf(ikm, out, salt=None, context=None, stream=None):
 def derive_keyset(ikm, salt=None, context=None, key_len=64, stream=None):
     """Per-packet keying from device rows (Identity.py:837-846): KeySet whose
     key i is Token(hkdf(key_len, ikm[i], salt[i], context)); derived and
-    expanded on the device."""
+    expanded on the device in one launch (the derived keys never reach HBM)
+    on ``stream``.  The key set is usable from any stream or host call right
+    away: every later launch that reads it waits for this build first."""
     _check_u8(ikm, salt, context)
     n = ikm.shape[0]
     lib = _native.load()

@@ -57,20 +57,32 @@ def partition(n, world, lengths=None):
 
 
 def _slice(buf, off, length, lo, hi):
-    """Bytes, rebased offsets and lengths of packets [lo, hi) of a packed batch."""
+    """Bytes, rebased offsets and lengths of packets [lo, hi) of a packed
+    batch.  Offsets need not ascend: the slice spans the range's lowest
+    offset to its highest end."""
     if hi <= lo:
         return buf.new_zeros(0), off.new_zeros(0), length.new_zeros(0)
-    start = int(off[lo])
-    end = int((off[lo:hi] + length[lo:hi].to(off.dtype)).max())
-    return buf[start:end], off[lo:hi] - start, length[lo:hi]
+    o = off[lo:hi].to(torch.int64)
+    start = int(o.min())
+    end = int((o + length[lo:hi].to(torch.int64)).max())
+    return buf[start:end], o - start, length[lo:hi].to(torch.int32)
 
 
-def scatter_packed(buf, off, length, bounds, src=0, group=None, device=None):
+def _wait(ops):
+    for req in (dist.batch_isend_irecv(ops) if ops else []):
+        req.wait()
+
+
+def scatter_packed(buf, off, length, bounds, src=0, group=None, device=None, rows=()):
     """Send each rank its packet range of a packed batch held on ``src``.
 
-    On the source, ``buf`` (uint8), ``off`` (int64) and ``length`` (int32)
-    describe the whole batch; elsewhere they are ignored (may be None).
-    Returns this rank's (buf, off, length) with offsets rebased to 0.
+    On the source, ``buf`` (uint8), ``off`` (any integer dtype, sent as
+    int64) and ``length`` (sent as int32) describe the whole batch, and each
+    tensor of ``rows`` holds one fixed-width record per packet (e.g. IVs
+    (n, 16) uint8, key indices (n,) int32); elsewhere they are ignored (may
+    be None; ``rows`` must then be ``(dtype, width)`` pairs so receivers can
+    size their buffers).  Returns this rank's (buf, off, length, rows) with
+    offsets rebased to 0.
     """
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     dev = device if device is not None else (buf.device if buf is not None else torch.device("cpu"))
@@ -86,55 +98,103 @@ def scatter_packed(buf, off, length, bounds, src=0, group=None, device=None):
         for r in range(world):
             if r == src:
                 continue
-            b, o, l = parts[r]
-            for t in (b, o, l):
+            lo, hi = bounds[r]
+            for t in (*parts[r], *(x[lo:hi] for x in rows)):
                 if t.numel():
                     ops.append(dist.P2POp(dist.isend, t.contiguous().to(dev), r, group))
-        for req in (dist.batch_isend_irecv(ops) if ops else []):
-            req.wait()
+        _wait(ops)
+        lo, hi = bounds[src]
         b, o, l = parts[src]
-        return b.to(dev), o.to(dev), l.to(dev)
+        return b.to(dev), o.to(dev), l.to(dev), [x[lo:hi].to(dev) for x in rows]
     rb = torch.empty(nb, dtype=torch.uint8, device=dev)
     ro = torch.empty(npk, dtype=torch.int64, device=dev)
     rl = torch.empty(npk, dtype=torch.int32, device=dev)
-    ops = [dist.P2POp(dist.irecv, t, src, group) for t in (rb, ro, rl) if t.numel()]
-    for req in (dist.batch_isend_irecv(ops) if ops else []):
-        req.wait()
-    return rb, ro, rl
+    rr = [torch.empty((npk, *w) if isinstance(w, tuple) else ((npk, w) if w else (npk,)), dtype=dt, device=dev)
+          for dt, w in rows]
+    _wait([dist.P2POp(dist.irecv, t, src, group) for t in (rb, ro, rl, *rr) if t.numel()])
+    return rb, ro, rl, rr
 
 
-def gather_packed(buf, off, length, dst=0, group=None):
-    """Mirror of scatter_packed: every rank sends its packed output range to
-    ``dst``, which returns the concatenated batch (offsets rebased per rank
-    onto one buffer, packet order = rank order).  Other ranks return None."""
+def gather_packed(buf, off, length, dst=0, group=None, rows=()):
+    """Mirror of scatter_packed: every rank sends its packed output range
+    (and its fixed-width ``rows``) to ``dst``, which returns the concatenated
+    batch (offsets rebased per rank onto one buffer, packet order = rank
+    order) and the concatenated rows.  Other ranks return None."""
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     dev = buf.device
+    off = off.to(torch.int64)
+    length = length.to(torch.int32)
     mine = torch.tensor([buf.numel(), off.numel()], dtype=torch.int64, device=dev)
     sizes = [torch.empty(2, dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(sizes, mine, group=group)
     sizes = [(int(s[0]), int(s[1])) for s in sizes]
     if rank != dst:
-        ops = [dist.P2POp(dist.isend, t.contiguous(), dst, group) for t in (buf, off, length) if t.numel()]
-        for req in (dist.batch_isend_irecv(ops) if ops else []):
-            req.wait()
+        _wait([dist.P2POp(dist.isend, t.contiguous(), dst, group) for t in (buf, off, length, *rows) if t.numel()])
         return None
-    bufs, offs, lens, ops = [], [], [], []
+    bufs, offs, lens, rws, ops = [], [], [], [[] for _ in rows], []
     for r in range(world):
         nb, npk = sizes[r]
         if r == dst:
-            b, o, l = buf, off, length
+            b, o, l, rr = buf, off, length, list(rows)
         else:
             b = torch.empty(nb, dtype=torch.uint8, device=dev)
             o = torch.empty(npk, dtype=torch.int64, device=dev)
             l = torch.empty(npk, dtype=torch.int32, device=dev)
-            ops += [dist.P2POp(dist.irecv, t, r, group) for t in (b, o, l) if t.numel()]
+            rr = [torch.empty((npk, *x.shape[1:]), dtype=x.dtype, device=dev) for x in rows]
+            ops += [dist.P2POp(dist.irecv, t, r, group) for t in (b, o, l, *rr) if t.numel()]
         bufs.append(b)
         offs.append(o)
         lens.append(l)
-    for req in (dist.batch_isend_irecv(ops) if ops else []):
-        req.wait()
+        for j, t in enumerate(rr):
+            rws[j].append(t)
+    _wait(ops)
     base, out_off = 0, []
     for r in range(world):
         out_off.append(offs[r] + base)
         base += sizes[r][0]
-    return torch.cat(bufs), torch.cat(out_off), torch.cat(lens)
+    return torch.cat(bufs), torch.cat(out_off), torch.cat(lens), [torch.cat(x) for x in rws]
+
+
+def sharded_call(work, buf, off, length, rows=(), row_specs=(), balance=False, src=0, group=None, device=None,
+                 sync=None):
+    """One batch held on ``src``, processed by every rank: partition (by
+    count, or by work_per_packet with ``balance``), scatter, ``work`` on each
+    rank's shard, gather back to ``src``.
+
+    ``work(buf, off, length, rows) -> (out_buf, out_off, out_len, out_rows)``
+    runs the per-rank kernels (reticulum_amd.device on a GPU; any stand-in
+    with the same contract in tests).  ``row_specs`` gives receivers the
+    (dtype, width) of each of ``rows``.  ``sync()`` (e.g.
+    torch.cuda.synchronize) separates the phases for timing.
+
+    Returns ``(result, times)``: on ``src`` result is the gathered
+    (buf, off, length, rows), elsewhere None; times = {"scatter_s",
+    "compute_s", "gather_s"} measured on this rank between barriers.
+    """
+    import time
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    sync = sync or (lambda: None)
+    if rank == src:
+        n = off.numel()
+        bounds = partition(n, world, length if balance else None)
+    else:
+        bounds = None
+    times = {}
+    dist.barrier(group=group)
+    t0 = time.perf_counter()
+    b, o, l, rr = scatter_packed(buf, off, length, bounds, src=src, group=group, device=device,
+                                 rows=rows if rank == src else row_specs)
+    sync()
+    dist.barrier(group=group)
+    t1 = time.perf_counter()
+    ob, oo, ol, orows = work(b, o, l, rr)
+    sync()
+    dist.barrier(group=group)
+    t2 = time.perf_counter()
+    res = gather_packed(ob, oo, ol, dst=src, group=group, rows=orows)
+    sync()
+    dist.barrier(group=group)
+    t3 = time.perf_counter()
+    times["scatter_s"], times["compute_s"], times["gather_s"] = t1 - t0, t2 - t1, t3 - t2
+    return res, times

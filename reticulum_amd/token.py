@@ -164,6 +164,19 @@ class KeySet:
         out, status, _ = self._decrypt_raw(tokens, key_idx)
         return out, status
 
+    def verify_batch(self, tokens, key_idx=None):
+        """Token.verify_hmac over many tokens (no AES, no plaintext written):
+        an int32 status array, RT_ST_OK where the tag verifies, RT_ST_BAD_HMAC
+        where it does not, RT_ST_TOO_SHORT for tokens of <= 32 bytes."""
+        toks = tokens if isinstance(tokens, Packed) else Packed.from_list(list(tokens))
+        n = len(toks)
+        kidx = self._key_idx(key_idx, n)
+        status = np.zeros(n, dtype=np.int32)
+        if n:
+            _native.check(self._lib.rt_verify_host(self._ptr, _ptr(toks.buf), _ptr(toks.off), _ptr(toks.length),
+                                                   _ptr(kidx), _ptr(status), n))
+        return status
+
     def verify_trials(self, tokens, candidates):
         """Identity.decrypt's ratchet loop (Identity.py:865-878) over a batch:
         ``candidates[t]`` lists key indices of this key set to try on token t,
@@ -296,8 +309,13 @@ class Token:
     def verify_hmac(self, token):                               # Token.py:77-84
         if len(token) <= 32:
             raise ValueError("Cannot verify HMAC on token of only " + str(len(token)) + " bytes")
-        st, _, _ = self._decrypt_one(bytes(token))
-        return st != RT_ST_BAD_HMAC
+        # the verify-only kernel: HMAC over token[:-32], no AES, no plaintext
+        ks = self.keyset
+        token = bytes(token)
+        st = ctypes.c_int32(-1)
+        _native.check(ks._lib.rt_verify_host(ks._ptr, token, _OFF0, ctypes.byref(ctypes.c_uint32(len(token))), None,
+                                             ctypes.byref(st), 1))
+        return st.value == RT_ST_OK
 
     def encrypt(self, data=None):                               # Token.py:87-97
         if not isinstance(data, bytes):

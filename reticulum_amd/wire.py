@@ -49,6 +49,7 @@ class _Dev:
         self.lib = _native.load()
         self.ctx = _native.context(device)
         self.bufs = []
+        self.keep = []          # host arrays an enqueued copy may still read
 
     def alloc(self, nbytes):
         p = self.lib.rt_device_alloc(self.ctx, max(int(nbytes), 1))
@@ -64,11 +65,16 @@ class _Dev:
         p = self.alloc(arr.nbytes)
         if arr.nbytes:
             _native.check(self.lib.rt_memcpy_h2d(self.ctx, p, arr.ctypes.data_as(ctypes.c_void_p), arr.nbytes, None))
+            self.keep.append(arr)
         return p
 
     def down(self, p, arr):
+        """Copy device bytes into arr and wait for them: the copy is an async
+        copy on the null stream, which HIP does not promise to complete
+        before returning for pageable memory."""
         if arr.nbytes:
             _native.check(self.lib.rt_memcpy_d2h(self.ctx, arr.ctypes.data_as(ctypes.c_void_p), p, arr.nbytes, None))
+            self.sync()
         return arr
 
     def sync(self):
@@ -78,6 +84,8 @@ class _Dev:
         return self
 
     def __exit__(self, *exc):
+        self.sync()
+        self.keep = []
         for p in self.bufs:
             self.lib.rt_device_free(self.ctx, p)
         self.bufs = []

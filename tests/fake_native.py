@@ -96,6 +96,24 @@ class FakeLib:
                 pbuf[region] = 0
         return 0
 
+    def rt_verify_host(self, ks, tok, tok_off, tok_len, key_idx, status, n):
+        """Token.verify_hmac per token: hashlib HMAC over token[:-32]."""
+        import hashlib
+        import hmac
+        self.calls.append(("verify", n))
+        keys = self._keysets[ks]
+        to, tl = _arr(tok_off, np.uint64, n), _arr(tok_len, np.uint32, n)
+        ki = _arr(key_idx, np.uint32, n)
+        tbuf, st = _arr(tok, np.uint8, int(max((to + tl).max(), 1))), _arr(status, np.int32, n)
+        for i in range(n):
+            k = keys[ki[i] if ki is not None else 0].tobytes()
+            t = tbuf[to[i]:to[i] + tl[i]].tobytes()
+            if len(t) <= 32:
+                st[i] = 1
+            else:
+                st[i] = 0 if hmac.new(k[:len(k) // 2], t[:-32], hashlib.sha256).digest() == t[-32:] else 2
+        return 0
+
     def rt_verify_trials_host(self, ks, tok, tok_off, tok_len, pair_off, pair_key, first, n_tok, n_pairs):
         """first[t] = rank of the first candidate key that opens token t
         (oracle status OK or BAD_PAD: tag verified over a well-formed token)."""

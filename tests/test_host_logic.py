@@ -128,3 +128,60 @@ def test_verify_trials_host_layer(fake):
         ks.verify_trials(toks[:2], cands[:1])
     with pytest.raises(ValueError):
         ks.verify_trials(toks[:1], [[len(keys)]])
+
+
+def test_verify_hmac_goldens_host_layer(golden, fake):
+    """verify_hmac runs the verify-only entry point (rt_verify_host, no
+    decrypt): True wherever the reference's tag check passes, including
+    tokens decrypt rejects afterwards (len40_validtag, ct_not_mult16)."""
+    for c in golden["decrypt"]:
+        t = rt.Token(b(c["key"]))
+        if c["status"] == 1:
+            with pytest.raises(ValueError):
+                t.verify_hmac(b(c["token"]))
+        else:
+            assert t.verify_hmac(b(c["token"])) is (c["status"] != 2), c["name"]
+    assert any(call[0] == "verify" for call in fake.calls)
+    assert not any(call[0] == "decrypt" for call in fake.calls)
+    ks = rt.KeySet(b(golden["decrypt"][0]["key"]))
+    st = ks.verify_batch([b(c["token"]) for c in golden["decrypt"] if c["key"] == golden["decrypt"][0]["key"]])
+    assert st.dtype == np.int32 and set(st.tolist()) <= {0, 1, 2}
+
+
+def test_device_api_validates_before_launch():
+    """reticulum_amd.device rejects rows narrower than the packet/token and
+    length/status/key arrays of the wrong dtype or size before any launch
+    (ADVICE r01): the kernels would otherwise write past a row or read int64
+    words as pairs of int32."""
+    import torch
+    from reticulum_amd import device
+    n, L = 4, 100
+    tl = rt.token_len(L)
+    ks = object()
+    pt = torch.zeros((n, L), dtype=torch.uint8)
+    iv = torch.zeros((n, 16), dtype=torch.uint8)
+    with pytest.raises(ValueError, match="tok rows"):
+        device.encrypt_uniform(ks, pt, L, iv, torch.zeros((n, tl - 1), dtype=torch.uint8))
+    with pytest.raises(ValueError, match="pt rows"):
+        device.encrypt_uniform(ks, pt[:, :50], L, iv, torch.zeros((n, tl), dtype=torch.uint8))
+    with pytest.raises(ValueError, match="tok rows"):
+        device.encrypt_uniform(ks, pt[:1], L, iv[:1], torch.zeros((1, 16), dtype=torch.uint8))
+    with pytest.raises(ValueError, match="key_idx"):
+        device.encrypt_uniform(ks, pt, L, iv, torch.zeros((n, tl), dtype=torch.uint8),
+                               key_idx=torch.zeros(n, dtype=torch.int64))
+    tok = torch.zeros((n, tl), dtype=torch.uint8)
+    ok32 = torch.zeros(n, dtype=torch.int32)
+    with pytest.raises(ValueError, match="pt rows"):
+        device.decrypt_uniform(ks, tok, tl, torch.zeros((n, tl - 49), dtype=torch.uint8), ok32, ok32)
+    with pytest.raises(ValueError, match="status"):
+        device.decrypt_uniform(ks, tok, tl, torch.zeros((n, tl - 48), dtype=torch.uint8), ok32,
+                               torch.zeros(n, dtype=torch.int64))
+    with pytest.raises(ValueError, match="key_idx"):
+        device.decrypt_uniform(ks, tok, tl, torch.zeros((n, tl - 48), dtype=torch.uint8), ok32, ok32,
+                               key_idx=torch.zeros(n + 1, dtype=torch.int32))
+    with pytest.raises(ValueError, match="pt_off"):
+        device.encrypt(ks, pt.reshape(-1), torch.zeros(n, dtype=torch.int32), ok32, iv, tok.reshape(-1),
+                       torch.zeros(n, dtype=torch.int64))
+    with pytest.raises(ValueError, match="tok_len"):
+        device.verify(ks, tok.reshape(-1), torch.zeros(n, dtype=torch.int64), torch.zeros(n, dtype=torch.int64),
+                      ok32)

@@ -59,7 +59,7 @@ def _worker(rank, world, port, result_q):
     obj = [bounds]
     dist.broadcast_object_list(obj, 0)
     bounds = obj[0]
-    b, o, l = shard.scatter_packed(tb, to, tl, bounds)
+    b, o, l, _ = shard.scatter_packed(tb, to, tl, bounds)
     # per-rank compute: one token per packet (IV = packet index bytes, deterministic)
     lo, hi = bounds[rank]
     toks = []
@@ -74,7 +74,7 @@ def _worker(rank, world, port, result_q):
     bout = torch.from_numpy(np.frombuffer(b"".join(toks), np.uint8).copy()) if toks else torch.zeros(0, dtype=torch.uint8)
     g = shard.gather_packed(bout, offs_out, lens_out)
     if rank == 0:
-        gb, go, gl = g
+        gb, go, gl, _ = g
         ok = len(gl) == 301
         for i in range(301):
             pt = buf[off[i]:off[i] + lens[i]].tobytes()
@@ -98,3 +98,81 @@ def test_scatter_compute_gather_gloo(world):
         p.join(timeout=300)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get() is True
+
+
+def _oracle_work(key):
+    """Per-rank stand-in for the device kernels with sharded_call's contract:
+    encrypt every packet of the shard under its IV row."""
+    from oracle import ctoken
+
+    def work(b, o, l, rows):
+        (ivs,) = rows
+        toks = [ctoken.encrypt(key, ivs[i].numpy().tobytes(), b[int(o[i]):int(o[i]) + int(l[i])].numpy().tobytes())
+                for i in range(len(o))]
+        lens = torch.tensor([len(t) for t in toks], dtype=torch.int32)
+        offs = torch.zeros(len(toks), dtype=torch.int64)
+        if len(toks) > 1:
+            offs[1:] = torch.cumsum(lens[:-1].to(torch.int64), 0)
+        out = torch.from_numpy(np.frombuffer(b"".join(toks), np.uint8).copy()) if toks else torch.zeros(0, torch.uint8)
+        return out, offs, lens, [torch.zeros(len(toks), dtype=torch.int32)]
+    return work
+
+
+def _sharded_worker(rank, world, port, result_q):
+    import torch.distributed as dist
+    from oracle import ctoken
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    key = bytes(range(64))
+    n = 257
+    if rank == 0:
+        rng = np.random.Generator(np.random.PCG64(78))
+        lens = rng.integers(0, 2000, n).astype(np.uint32)          # numpy Packed dtypes: uint32 lengths ...
+        off = np.zeros(n, np.uint64)                                 # ... and uint64 offsets
+        off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+        buf = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+        ivs = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+        args = (torch.from_numpy(buf), torch.from_numpy(off.astype(np.int64)), torch.from_numpy(lens.astype(np.int64)))
+        rows = [torch.from_numpy(ivs)]
+    else:
+        args, rows = (None, None, None), ()
+    res, times = shard.sharded_call(_oracle_work(key), *args, rows=rows, row_specs=[(torch.uint8, 16)],
+                                    balance=True)
+    assert set(times) == {"scatter_s", "compute_s", "gather_s"}
+    if rank == 0:
+        gb, go, gl, (gst,) = res
+        ok = len(gl) == n and gst.numel() == n and gl.dtype == torch.int32 and go.dtype == torch.int64
+        for i in range(n):
+            ref = ctoken.encrypt(key, ivs[i].tobytes(), buf[int(off[i]):int(off[i]) + int(lens[i])].tobytes())
+            ok = ok and gb[int(go[i]):int(go[i]) + int(gl[i])].numpy().tobytes() == ref
+        result_q.put(ok)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_call_gloo_world2():
+    """shard.sharded_call — the entry bench.py's sharded configs (c4, c5) run
+    over RCCL — end to end at world size 2 on gloo, the oracle standing in
+    for the per-rank kernels: work-balanced partition, scatter of bytes +
+    IV rows, gather of tokens + status rows, every token bit-exact."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get() is True
+
+
+def test_slice_handles_unordered_offsets():
+    buf = torch.arange(20, dtype=torch.uint8)
+    off = torch.tensor([10, 0, 5], dtype=torch.int64)
+    ln = torch.tensor([3, 4, 2], dtype=torch.int64)
+    b, o, l = shard._slice(buf, off, ln, 0, 3)
+    assert l.dtype == torch.int32 and o.dtype == torch.int64
+    for i in range(3):
+        assert b[int(o[i]):int(o[i]) + int(l[i])].tolist() == buf[int(off[i]):int(off[i]) + int(ln[i])].tolist()

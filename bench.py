@@ -7,13 +7,21 @@ of the batch (Token.encrypt, Token.py:87-97) followed by verify+decrypt of the
 tokens it produced (Token.decrypt, Token.py:100-114).  Inputs are generated on
 the device before timing (synthetic, uniform random bytes).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
 Multi-GPU: packets are independent, so each rank owns its own 2^20-packet
 shard (weak scaling) and no collective touches the data path; RCCL is used
 only for the barrier and the max-over-ranks reduction of the timings.
 Rank 0 prints one JSON line.
+
+--config c4 / c5 run BASELINE.json's sharded configs instead: rank 0 holds
+the whole batch (c4: 262 144 x 16 KiB Resource chunks, one key; c5: 8 M
+packets of 64 B-4 KiB, 65 536 keys, half encrypted and half decrypted), and
+shard.sharded_call moves each rank its share over RCCL (xGMI), runs the
+kernels, and gathers the outputs back; scatter, compute and gather are timed
+separately.  With N > 1 the default c2 run also makes one
+sharded c4 pass and reports it under "sharded_c4".
 """
 import argparse
 import json
@@ -61,7 +69,10 @@ def parse():
     ap.add_argument("--pt-stride", type=int, default=0, help="bytes between plaintext rows in HBM (0: packed)")
     ap.add_argument("--tok-stride", type=int, default=0, help="bytes between token rows in HBM (0: packed)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 disables)")
-    ap.add_argument("--cpu-workers", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-workers", type=int, default=0, help="0 = every CPU this process may run on")
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
+                    help="c2 (default) / c3: weak-scaling token steps; c4 / c5: sharded batch held by rank 0")
+    ap.add_argument("--sharded-reps", type=int, default=3, help="timed passes of a sharded config")
     ap.add_argument("--e2e", action="store_true", default=True, help="also time the PCIe-inclusive path")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false")
     return ap.parse_args()
@@ -75,7 +86,7 @@ def cpu_baseline(seconds, workers, L):
     import multiprocessing as mp
     from oracle import cpuref  # noqa: F401  (checked importable before forking)
     if workers <= 0:
-        workers = max(1, min(16, os.cpu_count() or 1))
+        workers = host_cpus()
     ctx = mp.get_context("spawn")
     with ctx.Pool(workers) as pool:
         t0 = time.perf_counter()
@@ -94,12 +105,41 @@ def cpu_baseline(seconds, workers, L):
     except OSError:
         pass
     return {
-        "value": rate, "unit": "packets/s", "gib_s": rate * L / 2**30, "cores": workers, "kind": "port",
+        "value": rate, "unit": "round trips/s (packets encrypted then decrypted)", "gib_s": rate * L / 2**30,
+        "cores": workers, "cpu_count": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "kind": "port",
         "sample": f"{pkts} round trips (encrypt+decrypt) of {L} B packets, one key, oracle/cpuref.py "
                   f"(pure Python, per-call key schedule like AES.py:83,100) on {workers} processes for "
                   f"~{seconds:.0f} s each; wall {wall:.1f} s; cpu '{model}'; cpuref/reference speed "
                   f"ratio measured in the build container: enc 1.64, dec 1.95 (tools/calibrate_cpuref.py)",
     }
+
+
+def host_cpus():
+    """The CPUs this process can actually use: its affinity mask, capped by
+    the cgroup CPU quota when one is set (cgroup v2 cpu.max, v1
+    cfs_quota/period).  A GPU box shows every core of the machine in
+    os.cpu_count() and the affinity mask while its container is given a
+    share; 256 workers on a 16-CPU share ran 38 % slower than 16 (r02d)."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(p)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                p = int(f.read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    if quota:
+        n = min(n, max(1, int(quota)))
+    return max(1, n)
 
 
 def _cpu_worker(arg):
@@ -135,6 +175,16 @@ def main():
 
     import reticulum_amd as rt
     from reticulum_amd import _native, device
+
+    if args.config in ("c4", "c5"):
+        res = sharded_bench(args.config, args, world, rank, local, reps=args.sharded_reps)
+        if rank == 0:
+            print(json.dumps(res))
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    if args.config == "c3" and args.keys == 1:
+        args.keys = 65536
 
     n, L = args.packets, args.length
     tl = rt.token_len(L)
@@ -213,6 +263,15 @@ def main():
     bytes_dec = n * (tl + (tl - 48) + 8)      # read token, write pt + len + status
     hbm_bytes = bytes_dec if dom == "decrypt" else bytes_enc
 
+    # c4 sharded over the same ranks (scatter / kernels / gather over RCCL):
+    # the xGMI legs of SURVEY §8(e), measured beside the weak-scaling headline
+    sharded = None
+    if world > 1 and os.environ.get("RNSTOK_BENCH_SHARDED", "1") != "0":
+        try:
+            sharded = sharded_bench("c4", args, world, rank, local, reps=2)
+        except Exception as e:  # reported, never fatal for the headline line
+            sharded = {"error": f"{type(e).__name__}: {e}"}
+
     if world > 1:
         dist.barrier()
     if rank != 0:
@@ -224,9 +283,9 @@ def main():
     pkts_total = n * world * args.steps
     value = pkts_total / elapsed
     line = {
-        "metric": "device-resident packets/s + GiB/s AES-256-CBC+HMAC-SHA256 at 1/2/4/8 MI355X",
+        "metric": BASELINE_METRIC,
         "value": value,
-        "unit": "packets/s",
+        "unit": "packets/s (round trips: each packet encrypted+MACed, then verified+decrypted)",
         "gib_s": value * L / 2**30,
         "n_gpus": world,
         "steps": args.steps,
@@ -276,10 +335,206 @@ def main():
                              "plus the VALU time of its instruction mix (DESIGN.md §4.5)"},
         "cpu_baseline": cpu,
         "e2e_pcie": e2e,
+        "sharded_c4": sharded,
     }
     print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def sharded_bench(cfg, args, world, rank, local, reps=3):
+    """BASELINE.json configs c4 / c5: one batch held by rank 0, sharded over
+    the ranks with shard.sharded_call (RCCL grouped point-to-point sends over
+    xGMI), per-rank kernels, gather back to rank 0.  Times are max over ranks
+    of each phase, averaged over `reps` passes after one warm-up pass; the
+    gathered outputs are checked on rank 0 (round trip)."""
+    import torch
+    import torch.distributed as dist
+    import reticulum_amd as rt
+    from reticulum_amd import device, shard
+
+    dev = torch.device("cuda", local)
+    dist_on = dist.is_available() and dist.is_initialized()
+    g = torch.Generator(device=dev).manual_seed(4242)
+    kg = torch.Generator().manual_seed(4243)
+    if cfg == "c4":
+        n = args.packets if args.packets != 1 << 20 else 262_144
+        L = 16384
+        n_keys = 1
+        lens = torch.full((n,), L, dtype=torch.int32)
+    else:
+        n = args.packets if args.packets != 1 << 20 else 8 << 20
+        n_keys = 65536
+        lens = torch.randint(64, 4097, (n,), dtype=torch.int32, generator=kg)
+    keys = torch.randint(0, 256, (n_keys, 64), dtype=torch.uint8, generator=kg).numpy()
+    ks = rt.KeySet(keys if n_keys > 1 else keys[0].tobytes(), device=local)
+    uniform = cfg == "c4"
+
+    def offsets(lengths):
+        o = torch.zeros(lengths.numel(), dtype=torch.int64, device=lengths.device)
+        if lengths.numel() > 1:
+            o[1:] = torch.cumsum(lengths[:-1].to(torch.int64), 0)
+        return o
+
+    def tok_lengths(lengths):
+        return (16 + 16 * (lengths // 16 + 1) + 32).to(torch.int32)
+
+    def enc_work(b, o, l, rows):
+        iv, kidx = rows if n_keys > 1 else (rows[0], None)
+        tl = tok_lengths(l)
+        toff = offsets(tl)
+        tok = torch.empty(int(tl.to(torch.int64).sum()), dtype=torch.uint8, device=dev)
+        if l.numel():
+            if uniform:
+                m = l.numel()
+                device.encrypt_uniform(ks, b.view(m, L), L, iv, tok.view(m, -1), key_idx=kidx)
+            else:
+                device.encrypt(ks, b, o, l, iv, tok, toff, key_idx=kidx, sort=True)
+        return tok, toff, tl, []
+
+    def dec_work(b, o, l, rows):
+        kidx = rows[0] if n_keys > 1 else None
+        cap = (l - 48).clamp(min=0)
+        poff = offsets(cap)
+        pt = torch.empty(max(int(cap.to(torch.int64).sum()), 1), dtype=torch.uint8, device=dev)
+        ol = torch.empty(l.numel(), dtype=torch.int32, device=dev)
+        st = torch.empty(l.numel(), dtype=torch.int32, device=dev)
+        if l.numel():
+            if uniform:
+                m = l.numel()
+                T = int(l[0])
+                device.decrypt_uniform(ks, b.view(m, T), T, pt[:m * (T - 48)].view(m, T - 48), ol, st, key_idx=kidx)
+            else:
+                device.decrypt(ks, b, o, l, pt, poff, ol, st, key_idx=kidx, sort=True)
+        return pt, poff, cap.to(torch.int32), [ol, st]
+
+    def run(work, buf, off, ln, rows, specs):
+        if not dist_on:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = work(buf, off, ln, rows)
+            torch.cuda.synchronize()
+            return out, {"scatter_s": 0.0, "compute_s": time.perf_counter() - t0, "gather_s": 0.0}
+        return shard.sharded_call(work, buf, off, ln, rows=rows, row_specs=specs, balance=not uniform,
+                                  sync=torch.cuda.synchronize)
+
+    def max_times(t):
+        v = torch.tensor([t["scatter_s"], t["compute_s"], t["gather_s"]], dtype=torch.float64, device=dev)
+        if dist_on:
+            dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        return v.tolist()
+
+    # rank 0's batch (inputs resident in its HBM before timing)
+    if rank == 0:
+        lens_d = lens.to(dev)
+        off_d = offsets(lens_d)
+        pt_buf = torch.randint(0, 256, (int(lens.to(torch.int64).sum()),), dtype=torch.uint8, device=dev,
+                               generator=g)
+        iv_d = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
+        kidx_d = torch.randint(0, n_keys, (n,), dtype=torch.int32, device=dev, generator=g) if n_keys > 1 else None
+    phases = []
+    if cfg == "c4":
+        phases.append(("encrypt", enc_work))
+    else:                                         # c5: half the packets encrypted, half decrypted
+        phases += [("encrypt", enc_work), ("decrypt", dec_work)]
+    h = n if cfg == "c4" else n // 2
+    report = {"metric": BASELINE_METRIC, "config": {}, "n_gpus": world, "reps": reps, "phases": {}}
+    total = {"scatter_s": 0.0, "compute_s": 0.0, "gather_s": 0.0}
+    ok = True
+    for name, work in phases:
+        if rank == 0:
+            sel = slice(0, h) if name == "encrypt" else slice(h, n)
+            ln = lens_d[sel]
+            if name == "encrypt":
+                b0 = int(off_d[sel][0]) if h else 0
+                buf = pt_buf[b0:b0 + int(ln.to(torch.int64).sum())]
+                off = off_d[sel] - b0
+                rows = [iv_d[sel]] + ([kidx_d[sel]] if n_keys > 1 else [])
+            else:   # the decrypt half's tokens, made on rank 0 before timing
+                tl = tok_lengths(ln)
+                off = offsets(tl)
+                buf = torch.empty(int(tl.to(torch.int64).sum()), dtype=torch.uint8, device=dev)
+                b0 = int(off_d[sel][0])
+                device.encrypt(ks, pt_buf, off_d[sel], ln, iv_d[sel], buf, off, key_idx=kidx_d[sel], sort=True)
+                ln, src_off, src_len = tl, off_d[sel], lens_d[sel]
+                rows = [kidx_d[sel]]
+            torch.cuda.synchronize()
+        else:
+            buf = off = ln = None
+            rows = []
+        specs = ([(torch.uint8, 16)] + ([(torch.int32, 0)] if n_keys > 1 else [])) if name == "encrypt" \
+            else [(torch.int32, 0)]
+        sums = [0.0, 0.0, 0.0]
+        out = None
+        for r in range(reps + 1):
+            out, t = run(work, buf, off, ln, rows, specs)
+            m = max_times(t)
+            if r:
+                sums = [a + b for a, b in zip(sums, m)]
+        sc, co, ga = (x / reps for x in sums)
+        total["scatter_s"] += sc
+        total["compute_s"] += co
+        total["gather_s"] += ga
+        if rank == 0:
+            gb, go, gl, grows = out
+            if name == "encrypt":        # round trip of the gathered tokens on rank 0
+                cap = gl - 48
+                poff = offsets(cap)
+                back = torch.empty(int(cap.to(torch.int64).sum()), dtype=torch.uint8, device=dev)
+                ol = torch.empty(h, dtype=torch.int32, device=dev)
+                st = torch.empty(h, dtype=torch.int32, device=dev)
+                device.decrypt(ks, gb, go, gl, back, poff, ol, st, key_idx=rows[1] if n_keys > 1 else None,
+                               sort=not uniform)
+                torch.cuda.synchronize()
+                ok = ok and bool((st == 0).all()) and torch.equal(ol, ln.to(torch.int32))
+                if uniform:
+                    ok = ok and torch.equal(back.view(h, -1)[:, :L], buf.view(h, L))
+                else:
+                    idx = torch.arange(0, h, 997, device=dev)
+                    for i in idx.tolist()[:64]:
+                        ok = ok and torch.equal(back[int(poff[i]):int(poff[i]) + int(ln[i])],
+                                                buf[int(off[i]):int(off[i]) + int(ln[i])])
+            else:                        # gathered plaintexts == the originals
+                ol, st = grows
+                ok = ok and bool((st == 0).all()) and torch.equal(ol, src_len)
+                for i in range(0, n - h, 997):
+                    a = int(src_off[i])
+                    ok = ok and torch.equal(gb[int(go[i]):int(go[i]) + int(src_len[i])],
+                                            pt_buf[a:a + int(src_len[i])])
+        byts = int(lens[:h].to(torch.int64).sum()) if name == "encrypt" else int(lens[h:].to(torch.int64).sum())
+        report["phases"][name] = {"packets": h if name == "encrypt" else n - h, "plaintext_bytes": byts,
+                                  "scatter_ms": sc * 1e3, "compute_ms": co * 1e3, "gather_ms": ga * 1e3,
+                                  "device_resident_packets_s": (h if name == "encrypt" else n - h) / co,
+                                  "device_resident_gib_s": byts / co / 2**30,
+                                  "end_to_end_packets_s": (h if name == "encrypt" else n - h) / (sc + co + ga),
+                                  "xgmi_scatter_gb_s": None, "xgmi_gather_gb_s": None}
+    pkts = n
+    byts_all = int(lens.to(torch.int64).sum())
+    report.update({
+        "value": pkts / total["compute_s"], "unit": "packets/s (device-resident, all ranks, compute phase)",
+        "gib_s": byts_all / total["compute_s"] / 2**30,
+        "end_to_end_packets_s": pkts / (total["scatter_s"] + total["compute_s"] + total["gather_s"]),
+        "scatter_ms": total["scatter_s"] * 1e3, "compute_ms": total["compute_s"] * 1e3,
+        "gather_ms": total["gather_s"] * 1e3, "scaling": "strong", "ok": ok,
+        "data": "synthetic random plaintext, IVs and keys generated on rank 0's device",
+    })
+    report["config"] = {
+        "workload": ("c4: 262 144 x 16 KiB Resource chunks, one key, held by rank 0, sharded by count"
+                     if cfg == "c4" else "c5: 8 M packets of 64 B-4 KiB, 65 536 keys, 50/50 encrypt/decrypt, "
+                                          "held by rank 0, sharded by AES+SHA work"),
+        "packets": n, "parallelism": f"shard{world} (RCCL point-to-point scatter/gather)" if dist_on else "1 GPU"}
+    if dist_on and world > 1:
+        moved = byts_all * (world - 1) / world
+        report["xgmi_note"] = (f"rank 0 sends {(world - 1)}/{world} of the inputs and receives {(world - 1)}/{world} "
+                               f"of the outputs: ~{moved / 1e9:.2f} GB each way")
+        for name in report["phases"]:
+            ph = report["phases"][name]
+            ph["xgmi_scatter_gb_s"] = ph["plaintext_bytes"] * (world - 1) / world / (ph["scatter_ms"] * 1e-3) / 1e9
+            ph["xgmi_gather_gb_s"] = ph["plaintext_bytes"] * (world - 1) / world / (ph["gather_ms"] * 1e-3) / 1e9
+    return report
+
+
+BASELINE_METRIC = "device-resident packets/s + GiB/s AES-256-CBC+HMAC-SHA256 at 1/2/4/8 MI355X"
 
 
 def _newest_pmc(kernel, n, L, keys):

@@ -13,6 +13,7 @@ shadowed by the class (RNS/Cryptography/__init__.py:38).
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
 """
+import ast
 import hashlib
 import json
 import os
@@ -170,7 +171,8 @@ def main():
     for line in src.splitlines():
         s = line.strip()
         if s.startswith("encrypted_message =") or s.startswith("fixed_token ="):
-            exec(s, ns)  # two string literals (data only)
+            name, rhs = s.split("=", 1)            # a literal only: never executed
+            ns[name.strip()] = ast.literal_eval(rhs.strip())
     fixed_key0 = src.split('fixed_keys = [')[1].split('("')[1].split('"')[0]
     captured = []
     orig_init = Token.__init__

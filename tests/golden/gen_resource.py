@@ -25,6 +25,7 @@ import types
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))          # tests/ (tests_helpers)
 REF = os.environ.get("RNS_REFERENCE", "/root/reference")
 
 
@@ -69,7 +70,7 @@ def main():
            "resources": [], "collisions": []}
     RNS.Packet = StubPacket
     try:
-        for size in (1, 200, 431, 1000, 5000, 40000):
+        for size in (1, 200, 431, 1000, 5000, 12000):
             link = StubLink()
             data = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
             res = RNS.Resource(data, link, advertise=False, auto_compress=False)
@@ -98,18 +99,20 @@ def main():
             hashmap += mh
         return hashmap, None
 
-    for n_parts, dup in ((40, (5, 30)), (400, (10, 10 + guard)), (400, (10, 11 + guard)), (300, (299, 299)),
-                         (300, None)):
-        stream = bytearray(rng.integers(0, 256, n_parts * sdu - 17, dtype=np.uint8).tobytes())
-        if dup and dup[0] != dup[1]:
-            a, b = dup
-            stream[b * sdu:(b + 1) * sdu] = stream[a * sdu:(a + 1) * sdu]
+    # The streams are inputs we make, so they are stored as (seed, length,
+    # dup) and rebuilt by tests_helpers.collision_stream; the reference's
+    # outputs (map hashes, the break index) are stored in full.
+    from tests_helpers import collision_stream
+    for k, (n_parts, dup) in enumerate(((40, (5, 30)), (400, (10, 10 + guard)), (400, (10, 11 + guard)),
+                                        (300, (299, 299)), (300, None))):
+        seed = 4490 + k
+        stream = collision_stream(seed, n_parts * sdu - 17, dup, sdu)
         rh = rng.integers(0, 256, 4, dtype=np.uint8).tobytes()
         hm, col = ref_loop(bytes(stream), rh)
         full = b"".join(RNS.Resource.get_map_hash(types.SimpleNamespace(random_hash=rh), bytes(stream[i * sdu:(i + 1) * sdu]))
                         for i in range(-(-len(stream) // sdu)))
-        out["collisions"].append({"n_parts": n_parts, "dup": dup, "stream_seed_len": len(stream),
-                                  "stream": bytes(stream).hex(), "random_hash": rh.hex(), "first_collision": col,
+        out["collisions"].append({"n_parts": n_parts, "dup": dup, "seed": seed, "stream_len": len(stream),
+                                  "random_hash": rh.hex(), "first_collision": col,
                                   "hashmap_until_break": hm.hex(), "map_hashes": full.hex()})
 
     path = os.path.join(HERE, "resource_vectors.json")

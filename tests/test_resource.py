@@ -14,7 +14,7 @@ import pytest
 
 import reticulum_amd as rt
 from oracle import ctoken
-from tests_helpers import b
+from tests_helpers import b, collision_stream
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -22,7 +22,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 @pytest.fixture(scope="module")
 def rv():
     with open(os.path.join(HERE, "golden", "resource_vectors.json")) as f:
-        return json.load(f)
+        d = json.load(f)
+    for c in d["collisions"]:          # inputs are stored as (seed, length, dup)
+        c["stream"] = collision_stream(c["seed"], c["stream_len"], c["dup"], d["sdu_default"]).hex()
+    return d
 
 
 @pytest.fixture

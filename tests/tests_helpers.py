@@ -37,3 +37,16 @@ def trial_case(seed, n_tok=40, n_keys=12):
         cands.append(cand)
         expect.append(exp)
     return keys, toks, cands, np.array(expect)
+
+
+def collision_stream(seed, length, dup, sdu=464):
+    """The input stream of a Resource collision-guard fixture
+    (tests/golden/gen_resource.py): `length` seeded random bytes with part
+    dup[1] overwritten by a copy of part dup[0] (no copy when dup is None or
+    names one part)."""
+    import numpy as np
+    stream = bytearray(np.random.Generator(np.random.PCG64(seed)).integers(0, 256, length, dtype=np.uint8).tobytes())
+    if dup and dup[0] != dup[1]:
+        a, c = dup
+        stream[c * sdu:(c + 1) * sdu] = stream[a * sdu:(a + 1) * sdu]
+    return bytes(stream)

@@ -13,6 +13,15 @@ import json
 import sys
 
 
+def kernel_class(name):
+    """encrypt / decrypt (the c2 kernels, as bench.py expects), or the kernel's
+    own name for the others (long-token, verify, key setup, hkdf, ...)."""
+    base = name.replace("(anonymous namespace)::", "").split("(")[0].split("<")[0].replace("rnstok::", "").replace("void ", "").strip()
+    if base in ("k_encrypt", "k_decrypt"):
+        return base[2:]
+    return base
+
+
 def summarise(root):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     for f in glob.glob(root + "/pmc_*/run_counter_collection.csv"):
@@ -20,7 +29,7 @@ def summarise(root):
             k = r["Kernel_Name"]
             if "rnstok" not in k:
                 continue
-            k = "encrypt" if "encrypt" in k else ("decrypt" if "decrypt" in k else "key_setup")
+            k = kernel_class(k)
             agg[k][(r["Counter_Name"], r["Dispatch_Id"])] += float(r["Counter_Value"])
     out = {}
     for k, d in agg.items():

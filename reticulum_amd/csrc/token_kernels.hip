@@ -878,6 +878,319 @@ __global__ __launch_bounds__(1024) void k_decrypt_long(DecArgs a) {
     }
 }
 
+// ------------------------------------------- decrypt, long tokens (v2) --
+//
+// The same work as k_decrypt_long, with the HMAC chain's message schedule
+// moved off the chain.  A token's 257 compressions are one serial chain in
+// one lane; one wave issues at most one VALU instruction per ~4 cycles, so
+// the chain's time is its instruction count.  W[16..63] depends only on the
+// message, not on the state, so here producer waves compute W[t] + K[t] for
+// every block and hand it to the chain (consumer) waves through an LDS ring:
+// the chain issues 14 instructions per round instead of ~21.5 (rounds plus
+// schedule), i.e. ~35 % fewer.
+//
+//   waves 0-1  consumers: the HMAC chains of 64 tokens each (one per lane)
+//   waves 2-3  producers: the schedules of the same 64 tokens, one block ahead
+//   waves 4-   block-parallel CBC decryption of the batch's quads (as v1)
+//
+// Producer p and consumer p pair through two LDS counters (steps written,
+// steps consumed) with a two-slot ring; no workgroup barrier inside the
+// chain, so the AES waves never wait on it.  The LDS image makes room for the
+// 64 KiB ring: T0/T1 only (Td2 = rotl16(Td0), Td3 = rotl16(Td1), one
+// v_alignbit per column on the XOR of the two lookups) and a 16-replica InvS.
+#ifndef RNSTOK_DL2_AES_WAVES
+#define RNSTOK_DL2_AES_WAVES 12
+#endif
+#ifndef RNSTOK_DL2_PRIO_PRODUCERS
+#define RNSTOK_DL2_PRIO_PRODUCERS 1
+#endif
+constexpr uint32_t DL2_TOK = 128, DL2_AES_WAVES = RNSTOK_DL2_AES_WAVES, DL2_THREADS = 64u * (4u + DL2_AES_WAVES);
+constexpr uint32_t DL2_INVS = 0x10000;                       // 256 rows x 64 B: InvS[x]*0x01010101 x16
+constexpr uint32_t DL2_RING = 0x14000;                       // 2 slots x 16 quads x 128 tokens x 16 B
+constexpr uint32_t DL2_SLOT = 16u * DL2_TOK * 16u;           // 32 KiB
+constexpr uint32_t DL2_FLAGS = DL2_RING + 2u * DL2_SLOT;     // ready[2], done[2] (u32)
+constexpr uint32_t LDS_DL2_BYTES = DL2_FLAGS + 64u;
+
+__device__ void fill_tables_dl2(uint32_t *tab, const uint8_t *inv) {
+    const uint32_t lane = threadIdx.x & 31u;
+    for (uint32_t u = threadIdx.x; u < 512u; u += blockDim.x) {        // Td0, Td1 (region 0 only)
+        const uint32_t x = u & 255u, t = u >> 8;
+        const uint32_t v = rotl(td0(inv, x), 8 * (int)t);
+        uint32_t *row = tab + (x << 6) + (t << 5);
+#pragma unroll 8
+        for (uint32_t j = 0; j < 32u; ++j) row[(j + lane) & 31u] = v;
+    }
+    for (uint32_t x = threadIdx.x; x < 256u; x += blockDim.x) {
+        const uint32_t v = (uint32_t)inv[x] * 0x01010101u;
+        uint32_t *row = tab + (DL2_INVS >> 2) + (x << 4);
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; ++j) row[(j + lane) & 15u] = v;
+    }
+    if (threadIdx.x < 16u) tab[(DL2_FLAGS >> 2) + threadIdx.x] = 0u;
+    __syncthreads();
+}
+
+// InvS[byte K of s] from 64-B rows of 16 replicas (lane l reads replica l & 15)
+template <int K>
+__device__ __forceinline__ uint32_t invs16(uint32_t s, uint32_t lane_off) {
+    const uint32_t t = K == 0 ? (s << 6) : (s >> (8 * K - 6));
+    return lds(and_or(t, 0x3fc0u, lane_off), 0);
+}
+
+// Equivalent inverse cipher on 4 independent blocks with Td0/Td1 only:
+// Td2[x] ^ Td3[y] = rotl16(Td0[x] ^ Td1[y]).
+template <int NR>
+__device__ __forceinline__ void dec_quad_t01(u32x4 p[4], const u32x4 c[4], u32x4 chain, const uint32_t *dk,
+                                             const Lanes &L, uint32_t inv_off) {
+    uint32_t s[4][4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        s[b][0] = c[b].x ^ dk[0]; s[b][1] = c[b].y ^ dk[1]; s[b][2] = c[b].z ^ dk[2]; s[b][3] = c[b].w ^ dk[3];
+    }
+#pragma unroll
+    for (int r = 1; r < NR; ++r) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            uint32_t v[16];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                v[4 * j + 0] = lds(taddr<0, 0>(s[b][j], L), 0);
+                v[4 * j + 1] = lds(taddr<1, 0>(s[b][(j + 3) & 3], L), 128);
+                v[4 * j + 2] = lds(taddr<2, 0>(s[b][(j + 2) & 3], L), 0);
+                v[4 * j + 3] = lds(taddr<3, 0>(s[b][(j + 1) & 3], L), 128);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t hi = v[4 * j + 2] ^ v[4 * j + 3];
+                s[b][j] = xor3(v[4 * j], v[4 * j + 1], rotr(hi, 16)) ^ dk[4 * r + j];
+            }
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint32_t *t = s[b];
+        u32x4 o;
+        o.x = bfi(0x0000ffffu, bfi(0x000000ffu, invs16<0>(t[0], inv_off), invs16<1>(t[3], inv_off)),
+                  bfi(0x00ff0000u, invs16<2>(t[2], inv_off), invs16<3>(t[1], inv_off))) ^ dk[4 * NR + 0];
+        o.y = bfi(0x0000ffffu, bfi(0x000000ffu, invs16<0>(t[1], inv_off), invs16<1>(t[0], inv_off)),
+                  bfi(0x00ff0000u, invs16<2>(t[3], inv_off), invs16<3>(t[2], inv_off))) ^ dk[4 * NR + 1];
+        o.z = bfi(0x0000ffffu, bfi(0x000000ffu, invs16<0>(t[2], inv_off), invs16<1>(t[1], inv_off)),
+                  bfi(0x00ff0000u, invs16<2>(t[0], inv_off), invs16<3>(t[3], inv_off))) ^ dk[4 * NR + 2];
+        o.w = bfi(0x0000ffffu, bfi(0x000000ffu, invs16<0>(t[3], inv_off), invs16<1>(t[2], inv_off)),
+                  bfi(0x00ff0000u, invs16<2>(t[1], inv_off), invs16<3>(t[0], inv_off))) ^ dk[4 * NR + 3];
+        p[b] = o ^ (b == 0 ? chain : c[b - 1]);
+    }
+}
+
+typedef __attribute__((address_space(3))) uint32_t lds_word_t;
+typedef __attribute__((address_space(3))) u32x4 lds_quad_t;
+
+__device__ __forceinline__ void dl2_wait(uint32_t flag_addr, uint32_t v) {
+    lds_word_t *f = (lds_word_t *)(uintptr_t)flag_addr;
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ void dl2_signal(uint32_t flag_addr, uint32_t v) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");      // the wave's ring accesses are done
+    if ((threadIdx.x & 63u) == 0u)
+        __hip_atomic_store((lds_word_t *)(uintptr_t)flag_addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int NR>
+__global__ __launch_bounds__(DL2_THREADS) void k_decrypt_long2(DecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
+    fill_tables_dl2(tab_u32, a.sbox + 256);
+    const Lanes LN(threadIdx.x & 31u);
+    const uint32_t inv_off = DL2_INVS | (4u * (threadIdx.x & 15u));
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t T = a.uni_len, nb = (T - 48u) >> 4, nquads = (nb + 3u) >> 2, tbl = nb - 4u * (nquads - 1u);
+    const uint32_t M = T - 32u, full = M >> 6;                 // full >= 16 here
+#if defined(RNSTOK_DL2_PROBE_AES_ONLY)          // timing probes (wrong statuses): one side of the kernel only
+    const bool consumer = false, producer = false;
+    if (wave < 4u) {
+        __syncthreads();
+        __syncthreads();
+        for (uint32_t base = blockIdx.x * DL2_TOK + gridDim.x * DL2_TOK; base < a.n; base += gridDim.x * DL2_TOK) {
+            __syncthreads();
+            __syncthreads();
+        }
+        return;
+    }
+#else
+    const bool consumer = wave < 2u, producer = wave == 2u || wave == 3u;
+#endif
+    const uint32_t pair = wave & 1u;                            // consumer p <-> producer p: tokens 64p..64p+63
+#ifdef RNSTOK_DL2_PRIO
+    // the chain waves issue first when ready; the AES waves fill the gaps
+    if (consumer || (producer && RNSTOK_DL2_PRIO_PRODUCERS)) __builtin_amdgcn_s_setprio(RNSTOK_DL2_PRIO);
+#endif
+    const uint32_t ready_f = DL2_FLAGS + 4u * pair, done_f = DL2_FLAGS + 8u + 4u * pair;
+    Keys<NR, false> K;
+    if (!consumer && !producer) K.load(a.rec, REC_DEC);
+    const uint32_t aes_lanes = blockDim.x - 256u;
+
+    for (uint32_t base = blockIdx.x * DL2_TOK; base < a.n; base += gridDim.x * DL2_TOK) {
+        const uint32_t ntok = a.n - base < DL2_TOK ? a.n - base : DL2_TOK;
+        uint32_t aes_id = threadIdx.x - 256u;      // (static-stride A/B only)
+        (void)aes_id;
+        (void)aes_lanes;
+        const uint32_t slot_tok = pair * 64u + lane;            // this lane's column of the ring
+        uint32_t diff = 1;
+        if (producer) {
+            // tokens past the batch hash a copy of its last token (results unused)
+            const uint32_t t = base + (slot_tok < ntok ? slot_tok : ntok - 1u);
+            const uint8_t *Kt = a.tok + in_off(a.tok_off, a.tok_stride, a.order ? a.order[t] : t);
+            u32x4 b0 = ld16(Kt), b1 = ld16(Kt + 16), b2 = ld16(Kt + 32), b3 = ld16(Kt + 48);
+            for (uint32_t i = 0; i < full; ++i) {
+                uint32_t w[16];
+                sha_units(w, b0, b1, b2, b3);
+                if (i + 1 < full) {                             // next block requested before this schedule
+                    const uint8_t *B = Kt + 64ull * (i + 1);
+                    b0 = ld16(B); b1 = ld16(B + 16); b2 = ld16(B + 32); b3 = ld16(B + 48);
+                }
+                if (i >= 2u) dl2_wait(done_f, i - 1u);           // the consumer is done with slot i & 1
+                lds_quad_t *ring = (lds_quad_t *)(uintptr_t)(DL2_RING + (i & 1u) * DL2_SLOT) + slot_tok;
+                constexpr uint32_t Kc[64] = {
+                    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+                    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+                    0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+                    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+                    0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+                    0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+                    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+                    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    uint32_t wk[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int t4 = 4 * q + j;
+                        uint32_t wt;
+                        if (t4 < 16) {
+                            wt = w[t4];
+                        } else {
+                            const uint32_t w15 = w[(t4 + 1) & 15], w2 = w[(t4 + 14) & 15];
+                            const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+                            const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+                            wt = w[t4 & 15] = (w[t4 & 15] + s0 + w[(t4 + 9) & 15]) + s1;
+                        }
+                        wk[j] = wt + Kc[t4];
+                    }
+                    ring[q * DL2_TOK] = u32x4{wk[0], wk[1], wk[2], wk[3]};
+                }
+                dl2_signal(ready_f, i + 1u);
+            }
+        } else if (consumer) {
+            const uint32_t t = base + slot_tok;
+            const bool valid = slot_tok < ntok;
+            const uint8_t *Kt = a.tok + in_off(a.tok_off, a.tok_stride,
+                                               a.order ? a.order[valid ? t : base] : (valid ? t : base));
+            uint32_t h[8], opad[8];
+            load_uniform8(h, a.rec + REC_IPAD);
+            for (uint32_t i = 0; i < full; ++i) {
+                dl2_wait(ready_f, i + 1u);
+                const lds_quad_t *ring = (const lds_quad_t *)(uintptr_t)(DL2_RING + (i & 1u) * DL2_SLOT) + slot_tok;
+                uint32_t v[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = h[k];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const u32x4 wk4 = ring[q * DL2_TOK];
+                    const uint32_t wk[4] = {wk4.x, wk4.y, wk4.z, wk4.w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int r = 4 * q + j;
+                        const uint32_t A = v[(0 - r) & 7], B = v[(1 - r) & 7], C = v[(2 - r) & 7], D = v[(3 - r) & 7];
+                        const uint32_t E = v[(4 - r) & 7], F = v[(5 - r) & 7], G = v[(6 - r) & 7], H = v[(7 - r) & 7];
+                        const uint32_t t1 = (H + wk[j]) + xor3(rotr(E, 6), rotr(E, 11), rotr(E, 25)) + bfi(E, F, G);
+                        const uint32_t t2 = xor3(rotr(A, 2), rotr(A, 13), rotr(A, 22)) + maj3(A, B, C);
+                        v[(3 - r) & 7] = D + t1;
+                        v[(7 - r) & 7] = t1 + t2;
+                    }
+                }
+                dl2_signal(done_f, i + 1u);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) h[k] += v[k];
+            }
+            const uint32_t fu = (M - 64u * full) >> 4;
+            const u32x4 z = {0u, 0u, 0u, 0u};
+            const uint8_t *R = Kt + 64ull * full;
+            sha_final_units(h, fu, fu > 0 ? ld16(R) : z, fu > 1 ? ld16(R + 16) : z, fu > 2 ? ld16(R + 32) : z,
+                            (uint64_t)(64u + M) * 8u);
+            load_uniform8(opad, a.rec + REC_OPAD);
+            uint32_t tag[8];
+            hmac_outer(tag, h, opad);
+            const u32x4 r0 = ld16(Kt + M), r1 = ld16(Kt + M + 16);
+            diff = (r0.x ^ bswap(tag[0])) | (r0.y ^ bswap(tag[1])) | (r0.z ^ bswap(tag[2])) |
+                   (r0.w ^ bswap(tag[3])) | (r1.x ^ bswap(tag[4])) | (r1.y ^ bswap(tag[5])) |
+                   (r1.z ^ bswap(tag[6])) | (r1.w ^ bswap(tag[7]));
+        } else {
+            const uint32_t items = ntok * nquads;
+            // Items are taken 64 at a time from an LDS counter: the AES waves
+            // that share a SIMD with a chain wave get fewer issue slots and so
+            // take fewer items, and every SIMD finishes together (a static
+            // stride left the chain SIMDs last: fused time = the sum of the
+            // two sides).
+            lds_word_t *next = (lds_word_t *)(uintptr_t)(DL2_FLAGS + 16u);
+            for (;;) {
+#ifdef RNSTOK_DL2_STATIC
+                const uint32_t c0 = aes_id - lane;      // (static stride, A/B)
+                aes_id += aes_lanes;
+#else
+                uint32_t c0 = 0u;
+                if (lane == 0u) c0 = __hip_atomic_fetch_add(next, 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                c0 = __builtin_amdgcn_readfirstlane(c0);
+#endif
+#ifdef RNSTOK_DL2_PROBE_SHA_ONLY
+                break;
+#endif
+                if (c0 >= items) break;                 // wave-uniform
+                // the tail chunk's idle lanes skip the body but stay in the
+                // loop (a divergent `continue` let them re-enter the loop
+                // head without lane 0 and spin on chunk 0: hang at n = 1)
+                const uint32_t j = c0 + lane;
+                if (j < items) {
+                    const uint32_t t = base + j % ntok, q = j / ntok;
+                    const uint32_t p = a.order ? a.order[t] : t;
+                    const uint8_t *C = a.tok + in_off(a.tok_off, a.tok_stride, p) + 16 + 64ull * q;
+                    uint8_t *D = a.pt + in_off(a.pt_off, a.pt_stride, p) + 64ull * q;
+                    const uint32_t nbk = q + 1u == nquads ? tbl : 4u;
+                    const u32x4 z = {0u, 0u, 0u, 0u};
+                    u32x4 c[4], pp[4];
+                    c[0] = ld16(C);
+                    c[1] = nbk > 1 ? ld16(C + 16) : z;
+                    c[2] = nbk > 2 ? ld16(C + 32) : z;
+                    c[3] = nbk > 3 ? ld16(C + 48) : z;
+                    const u32x4 chain = ld16(C - 16);      // previous ciphertext block (the IV for q = 0)
+                    dec_quad_t01<NR>(pp, c, chain, K.rk, LN, inv_off);
+                    st16(D, pp[0]);
+                    if (nbk > 1) st16(D + 16, pp[1]);
+                    if (nbk > 2) st16(D + 32, pp[2]);
+                    if (nbk > 3) st16(D + 48, pp[3]);
+                }
+            }
+        }
+        __syncthreads();          // plaintext of every token of this batch is written; the ring is idle
+        if (consumer) {
+            const uint32_t t = base + slot_tok;
+            if (slot_tok < ntok) {
+                const uint32_t p = a.order ? a.order[t] : t;
+                uint8_t *O = a.pt + in_off(a.pt_off, a.pt_stride, p);
+                const uint32_t padn = O[16u * nb - 1u];       // PKCS7.unpad: n = data[-1]
+                const int32_t st = diff ? 2 : (padn > 16u ? 4 : 0);
+                const uint32_t outlen = st == 0 ? 16u * nb - padn : (st == 4 ? padn : 0u);
+                if (st != 0) {
+                    const u32x4 z = {0u, 0u, 0u, 0u};
+                    for (uint32_t i = 0; i < nb; ++i) st16(O + 16 * i, z);
+                }
+                a.status[p] = st;
+                a.out_len[p] = outlen;
+            }
+        }
+        if (threadIdx.x < 16u) tab_u32[(DL2_FLAGS >> 2) + threadIdx.x] = 0u;     // counters restart per batch
+        __syncthreads();
+    }
+}
+
 // --------------------------------------------------------- ratchet trials --
 //
 // Identity.decrypt (RNS/Identity.py:865-878) tries the receiver's ratchets in
@@ -1240,8 +1553,12 @@ template <int NR>
 static hipError_t launch_dec_long_nr(const DecArgs &a, int n_cu, hipStream_t s) {
     uint64_t grid = (a.n + 127ull) / 128ull;
     if (grid > (uint64_t)n_cu) grid = n_cu;
+#ifdef RNSTOK_DL_V1          // A/B: the schedule computed on the chain lanes
     hipLaunchKernelGGL((k_decrypt_long<NR>), dim3((unsigned)grid), dim3(64 * RNSTOK_DEC_LONG_WAVES), LDS_DEC_BYTES, s,
                        a);
+#else
+    hipLaunchKernelGGL((k_decrypt_long2<NR>), dim3((unsigned)grid), dim3(DL2_THREADS), LDS_DL2_BYTES, s, a);
+#endif
     return hipGetLastError();
 }
 
@@ -1281,6 +1598,8 @@ hipError_t configure_kernels() {
     RT_CFG((k_encrypt<10, true>), LDS_ENC_BYTES);
     RT_CFG((k_decrypt_long<14>), LDS_DEC_BYTES);
     RT_CFG((k_decrypt_long<10>), LDS_DEC_BYTES);
+    RT_CFG((k_decrypt_long2<14>), LDS_DL2_BYTES);
+    RT_CFG((k_decrypt_long2<10>), LDS_DL2_BYTES);
     RT_CFG((k_encrypt_long4<14>), LDS_ENC_LONG4_BYTES);
     RT_CFG((k_encrypt_long4<10>), LDS_ENC_LONG4_BYTES);
     RT_CFG((k_encrypt_long<14, false>), LDS_ENC_LONG_BYTES);

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--length", type=int, default=500)
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--keys", type=int, default=1)
+    ap.add_argument("--probe", action="store_true", help="timing probes: skip the round-trip assertion")
     args = ap.parse_args()
 
     import torch

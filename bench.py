@@ -324,15 +324,19 @@ def main():
                      "frac_of_measured_valu_peak": achieved / (n_cu * 4 * 64 / 2.74 * 2.4e9),
                      "sustained_clock_ghz": sustained_clock_ghz(dom, n, L, args.keys),
                      "lds_frac": n * blocks(L) * LDS_LOOKUPS_PER_BLOCK / (dom_ms * 1e-3) / peak_lds,
+                     "issue_model": issue_model(dom, n, L, args.keys, n_cu, dom_ms,
+                                                sustained_clock_ghz(dom, n, L, args.keys)),
                      "note": "achieved = canonical int32 VALU lane-ops per launch (SURVEY §8(d): 352/AES block, "
                              "1464/SHA-256 compression, +8 tag compare) / HIP-event kernel time; peak = CUs x 128 "
-                             "lanes x 2.4 GHz (full-rate VALU); measured_valu_peak = v_xor_b32 at 2.74 cycles per wave64 "
-                             "instruction per SIMD (tools/valu_peak.hip, DESIGN.md 4.5); sustained_clock_ghz from the "
-                             "committed PMC run (GRBM_GUI_ACTIVE / 8 XCDs / kernel-trace average); frac_of_survey_P uses BASELINE.md §5's P = CUs x 64 "
-                             "x 2.4 GHz; traffic = HBM bytes per launch from the committed rocprofv3 PMC summary "
-                             "(profiles/*_pmc.json, FETCH_SIZE x 2 + WRITE_SIZE; see traffic_detail.calibration). On gfx950 LDS lookups and VALU issue do not "
-                             "overlap (tools/overlap_probe.hip: their times add), so the kernel's floor is the LDS time "
-                             "plus the VALU time of its instruction mix (DESIGN.md §4.5)"},
+                             "lanes x 2.4 GHz (full-rate VALU, MI355X_MICROARCH.md); measured_valu_peak = v_xor_b32 at 2.74 cycles "
+                             "per wave64 instruction per SIMD (tools/valu_peak.hip); sustained_clock_ghz from the "
+                             "committed PMC run (GRBM_GUI_ACTIVE / 8 XCDs / kernel-trace average); frac_of_survey_P uses "
+                             "BASELINE.md §5's P = CUs x 64 x 2.4 GHz; traffic = HBM bytes per launch from the committed "
+                             "rocprofv3 PMC summary (profiles/*_pmc.json, FETCH_SIZE x 2 + WRITE_SIZE; see "
+                             "traffic_detail.calibration). issue_model = the kernel's own instruction mix priced with the "
+                             "per-instruction issue costs measured by tools/cost_probe.hip (half-rate v_perm/v_alignbit/"
+                             "v_add3 and SGPR-operand ops 4.24 cycles, full-rate 2.40, each LDS lookup ~1.7 SIMD-cycles of "
+                             "the waves beside it; LDS and VALU work overlap, DESIGN.md §4.5)"},
         "cpu_baseline": cpu,
         "e2e_pcie": e2e,
         "sharded_c4": sharded,
@@ -535,6 +539,30 @@ def sharded_bench(cfg, args, world, rank, local, reps=3):
 
 
 BASELINE_METRIC = "device-resident packets/s + GiB/s AES-256-CBC+HMAC-SHA256 at 1/2/4/8 MI355X"
+
+
+# Issue-cost model of the c2 kernels: SIMD-cycles per wave of
+# 64 packets of 500 B, single key, from the loop bodies' instruction mix
+# (tools/asm_mix.py on the round-2 ISA) priced with tools/cost_probe.hip's
+# measured costs (profiles/r02a_cost_probe.txt).
+ISSUE_CYCLES_PER_WAVE_PACKET_500B = {
+    # quad 0 (AES only) + 7 loop quads (AES + SHA) + 3 finishing compressions
+    "encrypt": (5083 + 1523) + 7 * (9888 + 1523) + 3 * 4827,
+    # 8 quads (AES + SHA of the same quad) + 2 finishing compressions
+    "decrypt": 8 * (10057 + 1523) + 2 * 4798,
+}
+
+
+def issue_model(kernel, n, L, keys, n_cu, ms, clock_ghz):
+    """Floor of the dominant kernel from its issue cost (c2 shape only)."""
+    if L != 500 or keys != 1 or not clock_ghz:
+        return None
+    waves_per_simd = n / 64 / (n_cu * 4)
+    cycles = ISSUE_CYCLES_PER_WAVE_PACKET_500B[kernel] * waves_per_simd
+    floor_ms = cycles / (clock_ghz * 1e9) * 1e3
+    return {"floor_cycles_per_simd": cycles, "clock_ghz": clock_ghz, "floor_ms": floor_ms,
+            "frac_of_issue_floor": floor_ms / ms,
+            "floor_ms_at_2p4ghz": cycles / 2.4e9 * 1e3}
 
 
 def _newest_pmc(kernel, n, L, keys):

@@ -171,7 +171,10 @@ def main():
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        import datetime
+        # a bounded timeout: a stuck collective ends the run instead of hanging it
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                timeout=datetime.timedelta(seconds=300))
 
     import reticulum_amd as rt
     from reticulum_amd import _native, device

@@ -766,123 +766,11 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
 
 // ---------------------------------------------------- decrypt, long tokens --
 //
-// Few, long tokens, one key, uniform length T (48 + 16*nb, nb >= 61): CBC
-// decryption is block-parallel, only the HMAC is a serial chain.  A 512-thread
-// workgroup serves 128 tokens: waves 0-1 run the HMAC chains (one token per
-// lane, reading the ciphertext straight from HBM), waves 2-7 decrypt the
-// tokens' quads as independent work items (4 blocks each).  After a barrier
-// the HMAC lanes read their token's last plaintext byte, set the status and
-// zero the region of any token that failed.
-template <int NR>
-__global__ __launch_bounds__(1024) void k_decrypt_long(DecArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
-    fill_tables<true>(tab_u32, a.sbox, a.sbox + 256);
-    const Lanes LN(threadIdx.x & 31u);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-#ifndef RNSTOK_DEC_LONG_SHA_LANES
-#define RNSTOK_DEC_LONG_SHA_LANES 64
-#endif
-    constexpr uint32_t TOK = 128, SHA_LANES = RNSTOK_DEC_LONG_SHA_LANES, SHA_WAVES = TOK / SHA_LANES;
-    const uint32_t T = a.uni_len, nb = (T - 48u) >> 4, nquads = (nb + 3u) >> 2, tbl = nb - 4u * (nquads - 1u);
-    const bool sha = wave < SHA_WAVES;
-#ifdef RNSTOK_DEC_LONG_PRIO
-    if (sha) __builtin_amdgcn_s_setprio(RNSTOK_DEC_LONG_PRIO);
-#endif
-    Keys<NR, false> K;
-    if (!sha) K.load(a.rec, REC_DEC);
-    const uint32_t aes_lanes = blockDim.x - SHA_WAVES * 64u, aes_id = threadIdx.x - SHA_WAVES * 64u;
-
-    for (uint32_t base = blockIdx.x * TOK; base < a.n; base += gridDim.x * TOK) {
-        const uint32_t ntok = a.n - base < TOK ? a.n - base : TOK;
-        uint32_t diff = 1;
-        if (sha) {
-            const uint32_t t = base + wave * SHA_LANES + lane;
-            if (lane < SHA_LANES && t < a.n) {
-                const uint32_t p = a.order ? a.order[t] : t;
-                const uint8_t *Kt = a.tok + in_off(a.tok_off, a.tok_stride, p);
-                uint32_t h[8], opad[8];
-                load_uniform8(h, a.rec + REC_IPAD);
-                load_uniform8(opad, a.rec + REC_OPAD);
-                const uint32_t M = T - 32u, full = M >> 6;       // full >= 16 here
-                u32x4 b0 = ld16(Kt), b1 = ld16(Kt + 16), b2 = ld16(Kt + 32), b3 = ld16(Kt + 48);
-                for (uint32_t i = 0; i < full; ++i) {
-                    uint32_t w[16];
-                    sha_units(w, b0, b1, b2, b3);
-                    if (i + 1 < full) {          // next block requested before this compression
-                        const uint8_t *B = Kt + 64ull * (i + 1);
-                        b0 = ld16(B); b1 = ld16(B + 16); b2 = ld16(B + 32); b3 = ld16(B + 48);
-                    }
-#ifndef RNSTOK_DL_PROBE_AES_ONLY          // timing probe: no HMAC chain (wrong statuses)
-                    sha256_compress(h, w);
-#else
-                    h[0] ^= w[0];
-#endif
-                }
-                const uint32_t fu = (M - 64u * full) >> 4;
-                const u32x4 z = {0u, 0u, 0u, 0u};
-                const uint8_t *R = Kt + 64ull * full;
-                sha_final_units(h, fu, fu > 0 ? ld16(R) : z, fu > 1 ? ld16(R + 16) : z, fu > 2 ? ld16(R + 32) : z,
-                                (uint64_t)(64u + M) * 8u);
-                uint32_t tag[8];
-                hmac_outer(tag, h, opad);
-                const u32x4 r0 = ld16(Kt + M), r1 = ld16(Kt + M + 16);
-                diff = (r0.x ^ bswap(tag[0])) | (r0.y ^ bswap(tag[1])) | (r0.z ^ bswap(tag[2])) |
-                       (r0.w ^ bswap(tag[3])) | (r1.x ^ bswap(tag[4])) | (r1.y ^ bswap(tag[5])) |
-                       (r1.z ^ bswap(tag[6])) | (r1.w ^ bswap(tag[7]));
-            }
-        } else {
-            Sha256 dummy;
-            const uint32_t items = ntok * nquads;
-            for (uint32_t j = aes_id; j < items; j += aes_lanes) {
-                const uint32_t t = base + j % ntok, q = j / ntok;
-                const uint32_t p = a.order ? a.order[t] : t;
-                const uint8_t *C = a.tok + in_off(a.tok_off, a.tok_stride, p) + 16 + 64ull * q;
-                uint8_t *D = a.pt + in_off(a.pt_off, a.pt_stride, p) + 64ull * q;
-                const uint32_t nbk = q + 1u == nquads ? tbl : 4u;
-                const u32x4 z = {0u, 0u, 0u, 0u};
-                u32x4 c[4], pp[4];
-                c[0] = ld16(C);
-                c[1] = nbk > 1 ? ld16(C + 16) : z;
-                c[2] = nbk > 2 ? ld16(C + 32) : z;
-                c[3] = nbk > 3 ? ld16(C + 48) : z;
-                const u32x4 chain = ld16(C - 16);      // previous ciphertext block (the IV for q = 0)
-#ifndef RNSTOK_DL_PROBE_SHA_ONLY          // timing probe: no block decryption (wrong plaintext)
-                dec_quad<NR, false>(pp, c, chain, K.rk, LN, dummy);
-#else
-                pp[0] = c[0] ^ chain; pp[1] = c[1]; pp[2] = c[2]; pp[3] = c[3];
-#endif
-                st16(D, pp[0]);
-                if (nbk > 1) st16(D + 16, pp[1]);
-                if (nbk > 2) st16(D + 32, pp[2]);
-                if (nbk > 3) st16(D + 48, pp[3]);
-            }
-        }
-        __syncthreads();          // plaintext of every token of this block is written
-        if (sha) {
-            const uint32_t t = base + wave * SHA_LANES + lane;
-            if (lane < SHA_LANES && t < a.n) {
-                const uint32_t p = a.order ? a.order[t] : t;
-                uint8_t *O = a.pt + in_off(a.pt_off, a.pt_stride, p);
-                const uint32_t padn = O[16u * nb - 1u];       // PKCS7.unpad: n = data[-1]
-                const int32_t st = diff ? 2 : (padn > 16u ? 4 : 0);
-                uint32_t outlen = st == 0 ? 16u * nb - padn : (st == 4 ? padn : 0u);
-                if (st != 0) {
-                    const u32x4 z = {0u, 0u, 0u, 0u};
-                    for (uint32_t i = 0; i < nb; ++i) st16(O + 16 * i, z);
-                }
-                a.status[p] = st;
-                a.out_len[p] = outlen;
-            }
-        }
-        __syncthreads();
-    }
-}
-
-// ------------------------------------------- decrypt, long tokens (v2) --
-//
-// The same work as k_decrypt_long, with the HMAC chain's message schedule
-// moved off the chain.  A token's 257 compressions are one serial chain in
-// one lane; one wave issues at most one VALU instruction per ~4 cycles, so
+// Few, long tokens, one key, uniform length T (48 + 16*nb, nb >= 61), e.g.
+// the 16 KiB Resource segments of c4 sharded 8 ways (128 per CU).  CBC
+// decryption is block-parallel; only the HMAC is a serial chain, with the
+// message schedule moved off it.  A token's 257 compressions are one serial
+// chain in one lane; one wave issues at most one VALU instruction per ~4 cycles, so
 // the chain's time is its instruction count.  W[16..63] depends only on the
 // message, not on the state, so here producer waves compute W[t] + K[t] for
 // every block and hand it to the chain (consumer) waves through an LDS ring:
@@ -891,7 +779,8 @@ __global__ __launch_bounds__(1024) void k_decrypt_long(DecArgs a) {
 //
 //   waves 0-1  consumers: the HMAC chains of 64 tokens each (one per lane)
 //   waves 2-3  producers: the schedules of the same 64 tokens, one block ahead
-//   waves 4-   block-parallel CBC decryption of the batch's quads (as v1)
+//   waves 4-   block-parallel CBC decryption of the batch's quads, taken 64
+//              at a time from an LDS counter (SIMD balance)
 //
 // Producer p and consumer p pair through two LDS counters (steps written,
 // steps consumed) with a two-slot ring; no workgroup barrier inside the
@@ -900,9 +789,6 @@ __global__ __launch_bounds__(1024) void k_decrypt_long(DecArgs a) {
 // v_alignbit per column on the XOR of the two lookups) and a 16-replica InvS.
 #ifndef RNSTOK_DL2_AES_WAVES
 #define RNSTOK_DL2_AES_WAVES 12
-#endif
-#ifndef RNSTOK_DL2_PRIO_PRODUCERS
-#define RNSTOK_DL2_PRIO_PRODUCERS 1
 #endif
 constexpr uint32_t DL2_TOK = 128, DL2_AES_WAVES = RNSTOK_DL2_AES_WAVES, DL2_THREADS = 64u * (4u + DL2_AES_WAVES);
 constexpr uint32_t DL2_INVS = 0x10000;                       // 256 rows x 64 B: InvS[x]*0x01010101 x16
@@ -1019,20 +905,12 @@ __global__ __launch_bounds__(DL2_THREADS) void k_decrypt_long2(DecArgs a) {
     const bool consumer = wave < 2u, producer = wave == 2u || wave == 3u;
 #endif
     const uint32_t pair = wave & 1u;                            // consumer p <-> producer p: tokens 64p..64p+63
-#ifdef RNSTOK_DL2_PRIO
-    // the chain waves issue first when ready; the AES waves fill the gaps
-    if (consumer || (producer && RNSTOK_DL2_PRIO_PRODUCERS)) __builtin_amdgcn_s_setprio(RNSTOK_DL2_PRIO);
-#endif
     const uint32_t ready_f = DL2_FLAGS + 4u * pair, done_f = DL2_FLAGS + 8u + 4u * pair;
     Keys<NR, false> K;
     if (!consumer && !producer) K.load(a.rec, REC_DEC);
-    const uint32_t aes_lanes = blockDim.x - 256u;
 
     for (uint32_t base = blockIdx.x * DL2_TOK; base < a.n; base += gridDim.x * DL2_TOK) {
         const uint32_t ntok = a.n - base < DL2_TOK ? a.n - base : DL2_TOK;
-        uint32_t aes_id = threadIdx.x - 256u;      // (static-stride A/B only)
-        (void)aes_id;
-        (void)aes_lanes;
         const uint32_t slot_tok = pair * 64u + lane;            // this lane's column of the ring
         uint32_t diff = 1;
         if (producer) {
@@ -1132,14 +1010,9 @@ __global__ __launch_bounds__(DL2_THREADS) void k_decrypt_long2(DecArgs a) {
             // two sides).
             lds_word_t *next = (lds_word_t *)(uintptr_t)(DL2_FLAGS + 16u);
             for (;;) {
-#ifdef RNSTOK_DL2_STATIC
-                const uint32_t c0 = aes_id - lane;      // (static stride, A/B)
-                aes_id += aes_lanes;
-#else
                 uint32_t c0 = 0u;
                 if (lane == 0u) c0 = __hip_atomic_fetch_add(next, 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 c0 = __builtin_amdgcn_readfirstlane(c0);
-#endif
 #ifdef RNSTOK_DL2_PROBE_SHA_ONLY
                 break;
 #endif
@@ -1546,19 +1419,11 @@ hipError_t launch_encrypt(const EncArgs &args, int nr, int n_cu, SpareQueue *spa
     if (took) spare->release(s);
     return e;
 }
-#ifndef RNSTOK_DEC_LONG_WAVES
-#define RNSTOK_DEC_LONG_WAVES 8
-#endif
 template <int NR>
 static hipError_t launch_dec_long_nr(const DecArgs &a, int n_cu, hipStream_t s) {
     uint64_t grid = (a.n + 127ull) / 128ull;
     if (grid > (uint64_t)n_cu) grid = n_cu;
-#ifdef RNSTOK_DL_V1          // A/B: the schedule computed on the chain lanes
-    hipLaunchKernelGGL((k_decrypt_long<NR>), dim3((unsigned)grid), dim3(64 * RNSTOK_DEC_LONG_WAVES), LDS_DEC_BYTES, s,
-                       a);
-#else
     hipLaunchKernelGGL((k_decrypt_long2<NR>), dim3((unsigned)grid), dim3(DL2_THREADS), LDS_DL2_BYTES, s, a);
-#endif
     return hipGetLastError();
 }
 
@@ -1596,8 +1461,6 @@ hipError_t configure_kernels() {
     RT_CFG((k_encrypt<14, true>), LDS_ENC_BYTES);
     RT_CFG((k_encrypt<10, false>), LDS_ENC_BYTES);
     RT_CFG((k_encrypt<10, true>), LDS_ENC_BYTES);
-    RT_CFG((k_decrypt_long<14>), LDS_DEC_BYTES);
-    RT_CFG((k_decrypt_long<10>), LDS_DEC_BYTES);
     RT_CFG((k_decrypt_long2<14>), LDS_DL2_BYTES);
     RT_CFG((k_decrypt_long2<10>), LDS_DL2_BYTES);
     RT_CFG((k_encrypt_long4<14>), LDS_ENC_LONG4_BYTES);

@@ -34,7 +34,12 @@ def main():
     n, L = args.packets, args.length
     tl = 16 + 16 * (L // 16 + 1) + 32
     g = torch.Generator(device="cuda").manual_seed(1)
-    pt = torch.randint(0, 256, (n, L), dtype=torch.uint8, device="cuda", generator=g)
+    # the plaintext rows sit in a buffer padded to 16-B units per packet, so
+    # a variant that reads whole 16-B units of every packet (e.g. a
+    # block-interleaved layout experiment) stays inside the allocation
+    pt_buf = torch.zeros(n * ((L + 15) // 16 * 16), dtype=torch.uint8, device="cuda")
+    pt = pt_buf[: n * L].view(n, L)
+    pt.copy_(torch.randint(0, 256, (n, L), dtype=torch.uint8, device="cuda", generator=g))
     iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
     keys = torch.randint(0, 256, (args.keys, 64), dtype=torch.uint8).numpy()
     kidx = torch.randint(0, args.keys, (n,), dtype=torch.int32, device="cuda", generator=g) if args.keys > 1 else None

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--keys", type=int, default=1)
     ap.add_argument("--probe", action="store_true", help="timing probes: skip the round-trip assertion")
+    ap.add_argument("--kidx", choices=["random", "zero", "seq", "sorted"], default="random",
+                    help="per-packet key pattern (with --keys > 1)")
     args = ap.parse_args()
 
     import torch
@@ -43,6 +45,12 @@ def main():
     iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
     keys = torch.randint(0, 256, (args.keys, 64), dtype=torch.uint8).numpy()
     kidx = torch.randint(0, args.keys, (n,), dtype=torch.int32, device="cuda", generator=g) if args.keys > 1 else None
+    if kidx is not None and args.kidx == "zero":
+        kidx.zero_()
+    elif kidx is not None and args.kidx == "seq":
+        kidx = (torch.arange(n, device="cuda", dtype=torch.int32) % args.keys).contiguous()
+    elif kidx is not None and args.kidx == "sorted":
+        kidx = kidx.sort().values.contiguous()
     variants = []
     for path in args.libs:
         lib = ctypes.CDLL(os.path.abspath(path))

@@ -130,7 +130,7 @@ def test_fuzz_encrypt_decrypt_verify_vs_oracle(rt, case):
                          dk.astype(np.uint32) if nk > 1 else None, want_pt, poff.astype(np.uint64), want_len,
                          want_st, threads=8)
     d_kidx = cu(dk) if nk > 1 else None
-    d_out = torch.zeros(psize, dtype=torch.uint8, device="cuda")
+    d_out = torch.full((psize,), 0xA5, dtype=torch.uint8, device="cuda")
     d_len = torch.full((m,), -7, dtype=torch.int32, device="cuda")
     d_st = torch.full((m,), -7, dtype=torch.int32, device="cuda")
     d_dbuf, d_doff, d_tlen = cu(dbuf), cu(doff), cu(tlen)
@@ -148,8 +148,12 @@ def test_fuzz_encrypt_decrypt_verify_vs_oracle(rt, case):
     assert np.array_equal(olen, want_len), "case %d: output lengths differ" % case
     assert {int(s) for s in st} >= {rt.RT_ST_OK, rt.RT_ST_BAD_HMAC}
     out = d_out.cpu().numpy()
-    for i in np.nonzero(st == rt.RT_ST_OK)[0]:
-        assert np.array_equal(out[poff[i]:poff[i] + olen[i]], want_pt[poff[i]:poff[i] + olen[i]]), (case, i)
+    for i in range(m):              # whole body (pad included) on OK, zeroed region otherwise
+        got = out[poff[i]:poff[i] + cap[i]]
+        if st[i] == rt.RT_ST_OK:
+            assert np.array_equal(got, want_pt[poff[i]:poff[i] + cap[i]]), (case, i)
+        else:
+            assert not got.any(), (case, i, int(st[i]))
     # the tag check alone: OK wherever the oracle got past the HMAC
     tag_ok = (want_st == rt.RT_ST_OK) | (want_st == rt.RT_ST_BAD_CT_LEN) | (want_st == rt.RT_ST_BAD_PAD)
     assert np.array_equal(vst == rt.RT_ST_OK, tag_ok), "case %d: verify disagrees" % case

@@ -73,6 +73,8 @@ def parse():
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2 (default) / c3: weak-scaling token steps; c4 / c5: sharded batch held by rank 0")
     ap.add_argument("--sharded-reps", type=int, default=3, help="timed passes of a sharded config")
+    ap.add_argument("--sharded-timeout", type=float, default=150.0,
+                    help="N > 1: seconds allowed for the sharded c4 pass after the headline")
     ap.add_argument("--e2e", action="store_true", default=True, help="also time the PCIe-inclusive path")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false")
     return ap.parse_args()
@@ -169,12 +171,20 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    # RNSTOK_BENCH_REHEARSE=1: every rank on GPU local % count over gloo, to
+    # rehearse the N > 1 control flow on a one-GPU box (not a measurement)
+    rehearse = os.environ.get("RNSTOK_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
         import datetime
         # a bounded timeout: a stuck collective ends the run instead of hanging it
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local),
-                                timeout=datetime.timedelta(seconds=300))
+        if rehearse:
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                    timeout=datetime.timedelta(seconds=300))
 
     import reticulum_amd as rt
     from reticulum_amd import _native, device
@@ -266,23 +276,7 @@ def main():
     bytes_dec = n * (tl + (tl - 48) + 8)      # read token, write pt + len + status
     hbm_bytes = bytes_dec if dom == "decrypt" else bytes_enc
 
-    # c4 sharded over the same ranks (scatter / kernels / gather over RCCL):
-    # the xGMI legs of SURVEY §8(e), measured beside the weak-scaling headline
-    sharded = None
-    if world > 1 and os.environ.get("RNSTOK_BENCH_SHARDED", "1") != "0":
-        try:
-            sharded = sharded_bench("c4", args, world, rank, local, reps=2)
-        except Exception as e:  # reported, never fatal for the headline line
-            sharded = {"error": f"{type(e).__name__}: {e}"}
-
-    if world > 1:
-        dist.barrier()
-    if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
-        return
-
-    cpu = cpu_baseline(args.cpu_seconds, args.cpu_workers, L) if world == 1 else None
+    cpu = cpu_baseline(args.cpu_seconds, args.cpu_workers, L) if world == 1 and rank == 0 else None
     pkts_total = n * world * args.steps
     value = pkts_total / elapsed
     line = {
@@ -342,11 +336,60 @@ def main():
                              "the waves beside it; LDS and VALU work overlap, DESIGN.md §4.5)"},
         "cpu_baseline": cpu,
         "e2e_pcie": e2e,
-        "sharded_c4": sharded,
+        "sharded_c4": None,
     }
-    print(json.dumps(line))
+
+    # c4 sharded over the same ranks (scatter / kernels / gather over RCCL):
+    # the xGMI legs of SURVEY §8(e), measured beside the weak-scaling headline.
+    # Never fatal for the headline: an exception is reported in the line, and
+    # a pass that does not finish within --sharded-timeout (a stuck
+    # point-to-point transfer) makes rank 0 print the line with the error and
+    # every rank exit, before the process group's own 300 s timeout would
+    # abort the job without a line.
+    if world > 1 and os.environ.get("RNSTOK_BENCH_SHARDED", "1") != "0":
+        guard = _LineGuard(line if rank == 0 else None, args.sharded_timeout)
+        try:
+            line["sharded_c4"] = sharded_bench("c4", args, world, rank, local, reps=2)
+        except Exception as e:  # reported, never fatal for the headline line
+            line["sharded_c4"] = {"error": f"{type(e).__name__}: {e}"}
+        dist.barrier()
+        guard.finish()
+    elif world > 1:
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+class _LineGuard:
+    """Deadline for the optional sharded pass of an N > 1 run.  On expiry
+    rank 0 prints the headline line (sharded_c4 carrying the error) and every
+    rank leaves with status 0; finish() cancels it."""
+
+    def __init__(self, line, seconds):
+        import threading
+        self.line, self.lock, self.done = line, threading.Lock(), False
+        self.timer = threading.Timer(seconds, self._expire, args=(seconds,))
+        self.timer.daemon = True
+        self.timer.start()
+
+    def _expire(self, seconds):
+        with self.lock:
+            if self.done:
+                return
+            self.done = True
+            if self.line is not None:
+                prev = self.line.get("sharded_c4")
+                self.line["sharded_c4"] = {"error": f"sharded pass unfinished after {seconds} s", "partial": prev}
+                print(json.dumps(self.line), flush=True)
+            sys.stderr.flush()
+            os._exit(0)
+
+    def finish(self):
+        with self.lock:
+            self.done = True
+        self.timer.cancel()
 
 
 def sharded_bench(cfg, args, world, rank, local, reps=3):
@@ -423,7 +466,7 @@ def sharded_bench(cfg, args, world, rank, local, reps=3):
             torch.cuda.synchronize()
             return out, {"scatter_s": 0.0, "compute_s": time.perf_counter() - t0, "gather_s": 0.0}
         return shard.sharded_call(work, buf, off, ln, rows=rows, row_specs=specs, balance=not uniform,
-                                  sync=torch.cuda.synchronize)
+                                  device=dev, sync=torch.cuda.synchronize)
 
     def max_times(t):
         v = torch.tensor([t["scatter_s"], t["compute_s"], t["gather_s"]], dtype=torch.float64, device=dev)

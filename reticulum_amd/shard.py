@@ -68,9 +68,36 @@ def _slice(buf, off, length, lo, hi):
     return buf[start:end], o - start, length[lo:hi].to(torch.int32)
 
 
-def _wait(ops):
-    for req in (dist.batch_isend_irecv(ops) if ops else []):
+def _staged(group):
+    """gloo moves host tensors only: device tensors go through host copies
+    (the one-GPU rehearsal of bench.py's N > 1 path).  RCCL/NCCL moves them
+    directly over xGMI."""
+    return dist.get_backend(group) == "gloo"
+
+
+def _wait(ops, group=None):
+    """Post (kind, tensor, peer) transfers as one grouped batch and wait."""
+    if not ops:
+        return
+    stage = _staged(group)
+    posted, copy_back = [], []
+    for kind, t, peer in ops:
+        if stage and t.is_cuda:
+            h = t.cpu() if kind == "send" else torch.empty(t.shape, dtype=t.dtype)
+            if kind == "recv":
+                copy_back.append((t, h))
+            t = h
+        posted.append(dist.P2POp(dist.isend if kind == "send" else dist.irecv, t, peer, group))
+    for req in dist.batch_isend_irecv(posted):
         req.wait()
+    for t, h in copy_back:
+        t.copy_(h)
+
+
+def _default_device(group):
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
 
 
 def scatter_packed(buf, off, length, bounds, src=0, group=None, device=None, rows=()):
@@ -85,7 +112,7 @@ def scatter_packed(buf, off, length, bounds, src=0, group=None, device=None, row
     offsets rebased to 0.
     """
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    dev = device if device is not None else (buf.device if buf is not None else torch.device("cpu"))
+    dev = device if device is not None else (buf.device if buf is not None else _default_device(group))
     if rank == src:
         parts = [_slice(buf, off, length, lo, hi) for lo, hi in bounds]
         sizes = torch.tensor([[p[0].numel(), p[1].numel()] for p in parts], dtype=torch.int64, device=dev)
@@ -101,8 +128,8 @@ def scatter_packed(buf, off, length, bounds, src=0, group=None, device=None, row
             lo, hi = bounds[r]
             for t in (*parts[r], *(x[lo:hi] for x in rows)):
                 if t.numel():
-                    ops.append(dist.P2POp(dist.isend, t.contiguous().to(dev), r, group))
-        _wait(ops)
+                    ops.append(("send", t.contiguous().to(dev), r))
+        _wait(ops, group)
         lo, hi = bounds[src]
         b, o, l = parts[src]
         return b.to(dev), o.to(dev), l.to(dev), [x[lo:hi].to(dev) for x in rows]
@@ -111,7 +138,7 @@ def scatter_packed(buf, off, length, bounds, src=0, group=None, device=None, row
     rl = torch.empty(npk, dtype=torch.int32, device=dev)
     rr = [torch.empty((npk, *w) if isinstance(w, tuple) else ((npk, w) if w else (npk,)), dtype=dt, device=dev)
           for dt, w in rows]
-    _wait([dist.P2POp(dist.irecv, t, src, group) for t in (rb, ro, rl, *rr) if t.numel()])
+    _wait([("recv", t, src) for t in (rb, ro, rl, *rr) if t.numel()], group)
     return rb, ro, rl, rr
 
 
@@ -129,7 +156,7 @@ def gather_packed(buf, off, length, dst=0, group=None, rows=()):
     dist.all_gather(sizes, mine, group=group)
     sizes = [(int(s[0]), int(s[1])) for s in sizes]
     if rank != dst:
-        _wait([dist.P2POp(dist.isend, t.contiguous(), dst, group) for t in (buf, off, length, *rows) if t.numel()])
+        _wait([("send", t.contiguous(), dst) for t in (buf, off, length, *rows) if t.numel()], group)
         return None
     bufs, offs, lens, rws, ops = [], [], [], [[] for _ in rows], []
     for r in range(world):
@@ -141,13 +168,13 @@ def gather_packed(buf, off, length, dst=0, group=None, rows=()):
             o = torch.empty(npk, dtype=torch.int64, device=dev)
             l = torch.empty(npk, dtype=torch.int32, device=dev)
             rr = [torch.empty((npk, *x.shape[1:]), dtype=x.dtype, device=dev) for x in rows]
-            ops += [dist.P2POp(dist.irecv, t, r, group) for t in (b, o, l, *rr) if t.numel()]
+            ops += [("recv", t, r) for t in (b, o, l, *rr) if t.numel()]
         bufs.append(b)
         offs.append(o)
         lens.append(l)
         for j, t in enumerate(rr):
             rws[j].append(t)
-    _wait(ops)
+    _wait(ops, group)
     base, out_off = 0, []
     for r in range(world):
         out_off.append(offs[r] + base)

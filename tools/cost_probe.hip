@@ -103,6 +103,12 @@ KERNEL(k_pk_add_u16, "v_pk_add_u16 %0, %0, %1", "v")
 KERNEL(k_cndmask, "v_cndmask_b32 %0, %0, %2, vcc", "v")
 KERNEL(k_mov_dpp, "v_mov_b32_dpp %0, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf", "v")
 KERNEL(k_alignbit_s, "v_alignbit_b32 %0, %0, %0, %1", "s")
+// SDWA (round 2b): a byte of one register written into byte 1 of another,
+// the other bytes preserved: a T-table address (byte << 8 | lane) in one op
+KERNEL(k_sdwa_mov, "v_mov_b32_sdwa %0, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2", "v")
+KERNEL(k_sdwa_mov_self, "v_mov_b32_sdwa %0, %0 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2", "v")
+KERNEL(k_sdwa_mov_pad, "v_mov_b32_sdwa %0, %0 dst_sel:BYTE_1 dst_unused:UNUSED_PAD src0_sel:BYTE_2", "v")
+KERNEL(k_sdwa_xor, "v_xor_b32_sdwa %0, %0, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD", "v")
 
 // ---------------------------------------------------------------- part B --
 // 64 v_bitop3 (8 chains) plus NL lookups per iteration; the lookups' results
@@ -305,6 +311,10 @@ int main() {
     run("pk_add_u16 v,v", k_pk_add_u16, IA, 64, 0);
     run("cndmask v,v,vcc", k_cndmask, IA, 64, 0);
     run("mov_dpp quad_perm", k_mov_dpp, IA, 64, 0);
+    run("mov_sdwa byte2->byte1 preserve", k_sdwa_mov, IA, 64, 0);
+    run("mov_sdwa self preserve", k_sdwa_mov_self, IA, 64, 0);
+    run("mov_sdwa self pad", k_sdwa_mov_pad, IA, 64, 0);
+    run("xor_sdwa src0 byte2", k_sdwa_xor, IA, 64, 0);
     const int IB = 4000;
     printf("part B: 64 bitop3 + N ds_read_b32 (+N/2 sink bitop3) in every wave\n");
     run("mix N=0", k_mix<0>, IB, 64, 0);

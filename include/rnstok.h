@@ -120,7 +120,7 @@ int rt_encrypt(const rt_keyset *ks, const uint8_t *pt, const uint64_t *pt_off, c
                const uint32_t *key_idx, const uint8_t *iv, uint8_t *tok, const uint64_t *tok_off,
                uint32_t n, void *stream);
 /* Fixed-length batch: packet i at pt + i*pt_stride (pt_len bytes), token at
- * tok + i*tok_stride. */
+ * tok + i*tok_stride.  pt may be null when pt_len is 0. */
 int rt_encrypt_uniform(const rt_keyset *ks, const uint8_t *pt, uint64_t pt_stride, uint32_t pt_len,
                        const uint32_t *key_idx, const uint8_t *iv, uint8_t *tok, uint64_t tok_stride,
                        uint32_t n, void *stream);

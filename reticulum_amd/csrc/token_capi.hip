@@ -394,7 +394,8 @@ static int enc_common(const rt_keyset *k, EncArgs &a, void *stream) {
     int rc = check_keyset(k);
     if (rc) return rc;
     if (a.n == 0) return RT_OK;
-    if (!a.pt || !a.iv || !a.tok) return fail(RT_E_INVAL, "rt_encrypt: null buffer");
+    // a uniform batch of empty plaintexts reads no plaintext bytes
+    if ((!a.pt && (a.pt_len || a.uni_len)) || !a.iv || !a.tok) return fail(RT_E_INVAL, "rt_encrypt: null buffer");
     a.rec = k->d_rec;
     a.sbox = k->ctx->d_sbox;
     hipStream_t s = pick(k->ctx, stream);
@@ -660,6 +661,10 @@ int rt_encrypt_host(const rt_keyset *k, const uint8_t *pt, const uint64_t *pt_of
     a.pt = w + o_pt; a.pt_off = (const uint64_t *)(w + o_po); a.pt_len = (const uint32_t *)(w + o_pl);
     a.key_idx = key_idx ? (const uint32_t *)(w + o_ki) : nullptr; a.iv = w + o_iv;
     a.tok = w + o_tok; a.tok_off = (const uint64_t *)(w + o_to); a.n = n;
+    if (n == 1) {       // one packet (Token.encrypt): a uniform batch of one, so the latency-shaped kernels apply
+        a.pt += pt_off[0]; a.pt_off = nullptr; a.pt_len = nullptr; a.uni_len = pt_len[0];
+        a.tok += tok_off[0]; a.tok_off = nullptr;
+    }
     if ((rc = enc_common(k, a, s))) return rc;
     RT_HIP(hipMemcpyAsync(h ? h + o_tok : tok, w + o_tok, tok_ext, hipMemcpyDeviceToHost, s), "D2H tok");
     RT_HIP(hipStreamSynchronize(s), "stream sync");
@@ -721,6 +726,10 @@ int rt_decrypt_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_
     a.key_idx = key_idx ? (const uint32_t *)(w + o_ki) : nullptr; a.pt = w + o_pt;
     a.pt_off = (const uint64_t *)(w + o_po); a.out_len = (uint32_t *)(w + o_ol); a.status = (int32_t *)(w + o_st);
     a.n = n;
+    if (n == 1) {       // one token (Token.decrypt): a uniform batch of one
+        a.tok += tok_off[0]; a.tok_off = nullptr; a.tok_len = nullptr; a.uni_len = tok_len[0];
+        a.pt += pt_off[0]; a.pt_off = nullptr;
+    }
     if ((rc = dec_common(k, a, s))) return rc;
     if (h) {
         RT_HIP(hipMemcpyAsync(h + o_pt, w + o_pt, total - o_pt, hipMemcpyDeviceToHost, s), "D2H stage");

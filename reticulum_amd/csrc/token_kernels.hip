@@ -889,7 +889,7 @@ __global__ __launch_bounds__(DL2_THREADS) void k_decrypt_long2(DecArgs a) {
     const uint32_t inv_off = DL2_INVS | (4u * (threadIdx.x & 15u));
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     const uint32_t T = a.uni_len, nb = (T - 48u) >> 4, nquads = (nb + 3u) >> 2, tbl = nb - 4u * (nquads - 1u);
-    const uint32_t M = T - 32u, full = M >> 6;                 // full >= 16 here
+    const uint32_t M = T - 32u, full = M >> 6;                 // full = 0 for a 64-B token: no chain steps
 #if defined(RNSTOK_DL2_PROBE_AES_ONLY)          // timing probes (wrong statuses): one side of the kernel only
     const bool consumer = false, producer = false;
     if (wave < 4u) {
@@ -1375,10 +1375,19 @@ static hipError_t launch_enc_long_nr(const EncArgs &a, int n_cu, hipStream_t s) 
     return hipGetLastError();
 }
 
-// Long-token mode: uniform batches of >= 1 KiB packets that give each CU at
-// most two waves of packets in the one-lane-per-packet kernel.
-static bool use_long(uint32_t n, const uint32_t *len, uint32_t uni, int n_cu) {
-    return len == nullptr && uni >= 1024u && (uint64_t)n <= 128ull * (uint64_t)n_cu;
+// Long-token mode: uniform batches that give each CU at most two waves of
+// packets in the one-lane-per-packet kernel, where each lane's serial chain
+// (one instruction per ~4 cycles from a wave that has its SIMD nearly to
+// itself) is the whole launch.  The single-key kernels (k_encrypt_long4,
+// k_decrypt_long2) split every chain over lanes and waves and win at every
+// length there (2^15 x 500 B: encrypt 103 -> 58 us, decrypt 105 -> 49 us;
+// one 500-B packet: 91 -> 51 and 113 -> 34 us; profiles/r02v_lat.txt), so
+// they take any length; the per-key k_encrypt_long keeps its 1 KiB floor.
+#ifndef RNSTOK_LONG_MIN_LEN
+#define RNSTOK_LONG_MIN_LEN 0u
+#endif
+static bool use_long(uint32_t n, const uint32_t *len, uint32_t uni, int n_cu, uint32_t min_len) {
+    return len == nullptr && uni >= min_len && (uint64_t)n <= 128ull * (uint64_t)n_cu;
 }
 
 template <int NR>
@@ -1407,10 +1416,10 @@ static hipError_t balance(Args &a, Shape sh, SpareQueue *spare, hipStream_t s, b
 hipError_t launch_encrypt(const EncArgs &args, int nr, int n_cu, SpareQueue *spare, hipStream_t s) {
     EncArgs a = args;
 #ifndef RNSTOK_NO_LONG4
-    if (!a.key_idx && use_long(a.n, a.pt_len, a.uni_len, n_cu))
+    if (!a.key_idx && use_long(a.n, a.pt_len, a.uni_len, n_cu, RNSTOK_LONG_MIN_LEN))
         return nr == 14 ? launch_enc_long4_nr<14>(a, n_cu, s) : launch_enc_long4_nr<10>(a, n_cu, s);
 #endif
-    if (use_long(a.n, a.pt_len, a.uni_len, n_cu))
+    if (use_long(a.n, a.pt_len, a.uni_len, n_cu, 1024u))
         return nr == 14 ? launch_enc_long_nr<14>(a, n_cu, s) : launch_enc_long_nr<10>(a, n_cu, s);
     const Shape sh = shape_for(a.n, a.key_idx ? WG_PERKEY_ENC : WG_ENC, n_cu);
     bool took = false;
@@ -1429,8 +1438,10 @@ static hipError_t launch_dec_long_nr(const DecArgs &a, int n_cu, hipStream_t s) 
 
 hipError_t launch_decrypt(const DecArgs &args, int nr, int n_cu, SpareQueue *spare, hipStream_t s) {
     DecArgs a = args;
-    // long mode: one key, uniform well-formed tokens of >= 1 KiB body, few per CU
-    if (!a.key_idx && a.tok_len == nullptr && a.uni_len >= 48u + 1024u && ((a.uni_len - 48u) & 15u) == 0 &&
+    // long mode: one key, uniform well-formed tokens (whole blocks, at least
+    // one), few per CU
+    if (!a.key_idx && a.tok_len == nullptr && a.uni_len >= 64u && a.uni_len >= 48u + RNSTOK_LONG_MIN_LEN &&
+        ((a.uni_len - 48u) & 15u) == 0 &&
         (uint64_t)a.n <= 128ull * (uint64_t)n_cu)
         return nr == 14 ? launch_dec_long_nr<14>(a, n_cu, s) : launch_dec_long_nr<10>(a, n_cu, s);
     // one key and one pass at up to 1024 threads: the 1024-thread instance

@@ -356,7 +356,11 @@ def test_sorted_small_batches_chunk_edges(rt, n, n_keys, klen):
 
 @pytest.mark.parametrize("n,L,klen", [(300, 1024, 64), (300, 1500, 64), (20000, 4095, 64), (2048, 16391, 64),
                                        (1, 1024, 64), (129, 1039, 64), (257, 1036, 64), (300, 2047, 32),
-                                       (5000, 1055, 32), (64, 1064, 64)])
+                                       (5000, 1055, 32), (64, 1064, 64),
+                                       # short packets take the single-key long kernels too (round 2)
+                                       (1, 0, 64), (1, 15, 64), (3, 16, 64), (129, 17, 64), (300, 100, 32),
+                                       (1, 500, 64), (64, 500, 64), (32768, 500, 64), (257, 63, 64),
+                                       (5, 1023, 32), (2, 47, 32), (200, 48, 64)])
 def test_long_token_mode_vs_oracle(rt, n, L, klen):
     """Uniform batches of long tokens with few packets per CU take the
     long-token kernels (single key: a quad of lanes per CBC chain, AES waves
@@ -367,11 +371,13 @@ def test_long_token_mode_vs_oracle(rt, n, L, klen):
     from reticulum_amd import device
     rng = np.random.Generator(np.random.PCG64(L + n))
     tl = rt.token_len(L)
-    pt_h = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    pt_h = rng.integers(0, 256, (n, L + 1), dtype=np.uint8)[:, :L]     # rows of L bytes, never a null pointer
     iv_h = rng.integers(0, 256, (n, 16), dtype=np.uint8)
     key = rng.integers(0, 256, klen, dtype=np.uint8)
     ks = rt.KeySet(key.tobytes())
-    pt = torch.from_numpy(pt_h).cuda()
+    pt = torch.from_numpy(np.ascontiguousarray(rng.integers(0, 1, (n, L + 1), dtype=np.uint8))).cuda()[:, :L]
+    pt.copy_(torch.from_numpy(np.ascontiguousarray(pt_h)))
+    pt_h = np.ascontiguousarray(pt_h)
     tok = torch.empty((n, tl), dtype=torch.uint8, device="cuda")
     device.encrypt_uniform(ks, pt, L, torch.from_numpy(iv_h).cuda(), tok)
     sel = np.unique(np.concatenate([np.arange(0, n, max(1, n // 40)), [n - 1]]))
@@ -386,8 +392,9 @@ def test_long_token_mode_vs_oracle(rt, n, L, klen):
     assert int(st.abs().sum()) == 0 and torch.equal(back[:, :L], pt)
 
 
+@pytest.mark.parametrize("m", [65, 1, 2, 5, 31])
 @pytest.mark.parametrize("klen", [64, 32])
-def test_long_decrypt_statuses(rt, klen):
+def test_long_decrypt_statuses(rt, klen, m):
     """Long-token decrypt (block-parallel AES + serial HMAC lanes): tokens with
     valid HMAC but a bad / zero / short pad byte, and tampered tokens, give the
     reference statuses (Token.py:103-114, PKCS7.unpad) and the same outputs as
@@ -397,7 +404,7 @@ def test_long_decrypt_statuses(rt, klen):
     import torch
     from reticulum_amd import device
     rng = np.random.Generator(np.random.PCG64(77 + klen))
-    n, m = 300, 65                            # body = 16*m bytes >= 1 KiB
+    n = 300                                   # body = 16*m bytes (1 KiB and up, and short ones)
     key = rng.integers(0, 256, klen, dtype=np.uint8)
     ks = rt.KeySet(key.tobytes())
     x = rng.integers(0, 256, (n, 16 * m), dtype=np.uint8)
@@ -412,7 +419,7 @@ def test_long_decrypt_statuses(rt, klen):
     for i in range(n):                       # drop the all-pad block, re-MAC: last byte of x is the pad byte
         body = fh[i, : 16 + 16 * m].tobytes()
         toks[i] = np.frombuffer(body + hm.new(sk, body, hashlib.sha256).digest(), np.uint8)
-    toks[7::11, 100] ^= 1                     # tampered ciphertext
+    toks[7::11, min(100, tl - 33)] ^= 1       # tampered ciphertext
     toks[9::13, -1] ^= 0x80                   # tampered tag
     tok = torch.from_numpy(toks).cuda()
 

@@ -39,7 +39,7 @@ def main():
     # the plaintext rows sit in a buffer padded to 16-B units per packet, so
     # a variant that reads whole 16-B units of every packet (e.g. a
     # block-interleaved layout experiment) stays inside the allocation
-    pt_buf = torch.zeros(n * ((L + 15) // 16 * 16), dtype=torch.uint8, device="cuda")
+    pt_buf = torch.zeros(max(n * ((L + 15) // 16 * 16), 16), dtype=torch.uint8, device="cuda")
     pt = pt_buf[: n * L].view(n, L)
     pt.copy_(torch.randint(0, 256, (n, L), dtype=torch.uint8, device="cuda", generator=g))
     iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)

@@ -1382,9 +1382,14 @@ static hipError_t launch_enc_long_nr(const EncArgs &a, int n_cu, hipStream_t s) 
 // k_decrypt_long2) split every chain over lanes and waves and win at every
 // length there (2^15 x 500 B: encrypt 103 -> 58 us, decrypt 105 -> 49 us;
 // one 500-B packet: 91 -> 51 and 113 -> 34 us; profiles/r02v_lat.txt), so
-// they take any length; the per-key k_encrypt_long keeps its 1 KiB floor.
+// they take any length.  So does the per-key k_encrypt_long (2^15 x 500 B
+// with 64 keys: 101 -> 80 us; x 1000 B: 172 -> 129 us; even at 100 B;
+// profiles/r02x_lat_perkey.txt).
 #ifndef RNSTOK_LONG_MIN_LEN
 #define RNSTOK_LONG_MIN_LEN 0u
+#endif
+#ifndef RNSTOK_LONG_PERKEY_MIN_LEN
+#define RNSTOK_LONG_PERKEY_MIN_LEN 0u
 #endif
 static bool use_long(uint32_t n, const uint32_t *len, uint32_t uni, int n_cu, uint32_t min_len) {
     return len == nullptr && uni >= min_len && (uint64_t)n <= 128ull * (uint64_t)n_cu;
@@ -1419,7 +1424,7 @@ hipError_t launch_encrypt(const EncArgs &args, int nr, int n_cu, SpareQueue *spa
     if (!a.key_idx && use_long(a.n, a.pt_len, a.uni_len, n_cu, RNSTOK_LONG_MIN_LEN))
         return nr == 14 ? launch_enc_long4_nr<14>(a, n_cu, s) : launch_enc_long4_nr<10>(a, n_cu, s);
 #endif
-    if (use_long(a.n, a.pt_len, a.uni_len, n_cu, 1024u))
+    if (use_long(a.n, a.pt_len, a.uni_len, n_cu, RNSTOK_LONG_PERKEY_MIN_LEN))
         return nr == 14 ? launch_enc_long_nr<14>(a, n_cu, s) : launch_enc_long_nr<10>(a, n_cu, s);
     const Shape sh = shape_for(a.n, a.key_idx ? WG_PERKEY_ENC : WG_ENC, n_cu);
     bool took = false;

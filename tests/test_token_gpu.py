@@ -392,6 +392,40 @@ def test_long_token_mode_vs_oracle(rt, n, L, klen):
     assert int(st.abs().sum()) == 0 and torch.equal(back[:, :L], pt)
 
 
+@pytest.mark.parametrize("n,L", [(1, 0), (3, 1), (100, 15), (100, 16), (129, 17), (64, 47), (65, 48), (300, 100),
+                                 (1, 500), (3000, 500), (200, 1000), (32768, 200)])
+def test_long_mode_per_key_short_vs_oracle(rt, n, L):
+    """Uniform batches with per-packet keys and few packets per CU take the
+    per-key long-token encrypt (a CBC chain per lane, hashing on waves of
+    their own) at every length: bit-exact vs the oracle, and decrypt (general
+    kernel) round-trips."""
+    import torch
+    from reticulum_amd import device
+    rng = np.random.Generator(np.random.PCG64(5 * L + n))
+    nk = 97
+    tl = rt.token_len(L)
+    pt_h = np.ascontiguousarray(rng.integers(0, 256, (n, L), dtype=np.uint8))
+    iv_h = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    keys = rng.integers(0, 256, (nk, 64), dtype=np.uint8)
+    kidx = rng.integers(0, nk, n).astype(np.int32)
+    ks = rt.KeySet(keys)
+    pt = torch.zeros((n, L + 1), dtype=torch.uint8, device="cuda")[:, :L]
+    pt.copy_(torch.from_numpy(pt_h))
+    d_k = torch.from_numpy(kidx).cuda()
+    tok = torch.empty((n, tl), dtype=torch.uint8, device="cuda")
+    device.encrypt_uniform(ks, pt, L, torch.from_numpy(iv_h).cuda(), tok, key_idx=d_k)
+    sel = np.unique(np.concatenate([np.arange(0, n, max(1, n // 40)), [n - 1]]))
+    ref, _, _ = _oracle_tokens(keys, pt_h[sel].reshape(-1), np.arange(len(sel), dtype=np.uint64) * L,
+                               np.full(len(sel), L, np.uint32), iv_h[sel], kidx[sel].astype(np.uint32))
+    assert np.array_equal(ref.reshape(len(sel), tl), tok.cpu().numpy()[sel])
+    back = torch.empty((n, tl - 48), dtype=torch.uint8, device="cuda")
+    ol = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    device.decrypt_uniform(ks, tok, tl, back, ol, st, key_idx=d_k)
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0 and torch.equal(back[:, :L], pt)
+
+
 @pytest.mark.parametrize("m", [65, 1, 2, 5, 31])
 @pytest.mark.parametrize("klen", [64, 32])
 def test_long_decrypt_statuses(rt, klen, m):

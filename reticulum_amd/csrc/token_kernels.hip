@@ -1426,6 +1426,7 @@ hipError_t launch_encrypt(const EncArgs &args, int nr, int n_cu, SpareQueue *spa
 #endif
     if (use_long(a.n, a.pt_len, a.uni_len, n_cu, RNSTOK_LONG_PERKEY_MIN_LEN))
         return nr == 14 ? launch_enc_long_nr<14>(a, n_cu, s) : launch_enc_long_nr<10>(a, n_cu, s);
+
     const Shape sh = shape_for(a.n, a.key_idx ? WG_PERKEY_ENC : WG_ENC, n_cu);
     bool took = false;
     hipError_t e = balance(a, sh, spare, s, &took);

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--probe", action="store_true", help="timing probes: skip the round-trip assertion")
     ap.add_argument("--kidx", choices=["random", "zero", "seq", "sorted"], default="random",
                     help="per-packet key pattern (with --keys > 1)")
+    ap.add_argument("--packed", type=int, default=-1,
+                    help="variable lengths drawn from [PACKED, length] through rt_encrypt/rt_decrypt (packed entry)")
     args = ap.parse_args()
 
     import torch
@@ -69,16 +71,31 @@ def main():
     s = torch.cuda.current_stream()
     sp = s.cuda_stream
     kp = kidx.data_ptr() if kidx is not None else None
+    packed = args.packed >= 0
+    if packed:
+        lens = torch.randint(args.packed, L + 1, (n,), dtype=torch.int32, device="cuda", generator=g)
+        rows = torch.arange(n, dtype=torch.int64, device="cuda")
+        p_off, t_off, b_off = rows * L, rows * tl, rows * (tl - 48)
+        t_len = (16 + 16 * (lens // 16 + 1) + 32).to(torch.int32)
 
     def run(v, ev=None):
         if ev:
             ev[0].record(s)
-        rc = v["lib"].rt_encrypt_uniform(v["ks"], pt.data_ptr(), L, L, kp, iv.data_ptr(), v["tok"].data_ptr(), tl, n, sp)
+        if packed:
+            rc = v["lib"].rt_encrypt(v["ks"], pt_buf.data_ptr(), p_off.data_ptr(), lens.data_ptr(), kp, iv.data_ptr(),
+                                     v["tok"].data_ptr(), t_off.data_ptr(), n, sp)
+        else:
+            rc = v["lib"].rt_encrypt_uniform(v["ks"], pt.data_ptr(), L, L, kp, iv.data_ptr(), v["tok"].data_ptr(), tl,
+                                             n, sp)
         assert rc == 0
         if ev:
             ev[1].record(s)
-        rc = v["lib"].rt_decrypt_uniform(v["ks"], v["tok"].data_ptr(), tl, tl, kp, v["back"].data_ptr(), tl - 48,
-                                         v["ol"].data_ptr(), v["st"].data_ptr(), n, sp)
+        if packed:
+            rc = v["lib"].rt_decrypt(v["ks"], v["tok"].data_ptr(), t_off.data_ptr(), t_len.data_ptr(), kp,
+                                     v["back"].data_ptr(), b_off.data_ptr(), v["ol"].data_ptr(), v["st"].data_ptr(), n, sp)
+        else:
+            rc = v["lib"].rt_decrypt_uniform(v["ks"], v["tok"].data_ptr(), tl, tl, kp, v["back"].data_ptr(), tl - 48,
+                                             v["ol"].data_ptr(), v["st"].data_ptr(), n, sp)
         assert rc == 0
         if ev:
             ev[2].record(s)
@@ -88,8 +105,17 @@ def main():
         run(v)
     torch.cuda.synchronize()
     for v in variants:
-        ok = bool((v["st"] == 0).all()) and torch.equal(v["back"][:, :L], pt)
-        same = torch.equal(v["tok"], variants[0]["tok"])
+        if packed:
+            ok = bool((v["st"] == 0).all()) and torch.equal(v["ol"], lens)
+            for i in range(0, n, max(1, n // 64)):
+                ok = ok and torch.equal(v["back"][i, :int(lens[i])], pt[i, :int(lens[i])])
+        else:
+            ok = bool((v["st"] == 0).all()) and torch.equal(v["back"][:, :L], pt)
+        if packed:     # token bytes only (rows are wider than their tokens)
+            same = all(torch.equal(v["tok"][i, :int(t_len[i])], variants[0]["tok"][i, :int(t_len[i])])
+                       for i in range(0, n, max(1, n // 256)))
+        else:
+            same = torch.equal(v["tok"], variants[0]["tok"])
         print(f"{v['path']}: round-trip ok={ok} tokens==variant0: {same}")
     for r in range(args.rounds):
         for v in (variants if r % 2 == 0 else variants[::-1]):

@@ -1,6 +1,8 @@
 #!/bin/bash
 # IFAC kernel variants: fenced compressions (fewer VGPRs, 5 waves/SIMD), and
 # forced occupancy.  One process per variant through RNSTOK_LIB, twice each.
+# (RNSTOK_IFAC_FENCED / RNSTOK_IFAC_WAVES lived in the experimental k_ifac only;
+# the tree kept the original kernel after this A/B.)
 set -o pipefail
 mkdir -p gpurun_out
 F="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-result -Wno-unused-value"

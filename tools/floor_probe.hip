@@ -13,7 +13,8 @@
 //                compression of the previous quad), the ciphertext fed back
 //                as the next plaintext and as the next SHA block
 //   core_enc0  : enc_quad<14, false> (quad 0 of a packet: AES chain only)
-//   core_dec   : dec_quad<14, true> (4 independent blocks + one compression)
+//   core_dec   : dec_quad<14, true> (4 independent blocks + one compression),
+//                at 768 threads (the c2 kernel's shape) and at 1024
 //   core_sha   : sha256_compress alone (hmac_finish's compressions)
 //
 // Per c2 wave-packet (64 packets of 500 B): encrypt = 1 x core_enc0 + 7 x
@@ -104,7 +105,8 @@ __global__ __launch_bounds__(1024) void k_core_enc(const uint32_t *rec, uint32_t
     STAMP_END(acc)
 }
 
-__global__ __launch_bounds__(768) void k_core_dec(const uint32_t *rec, uint32_t *out, Stamp *st, uint32_t seed, int iters) {
+template <int WG>
+__global__ __launch_bounds__(WG) void k_core_dec(const uint32_t *rec, uint32_t *out, Stamp *st, uint32_t seed, int iters) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
     fill_any(tab, LDS_DEC_BYTES / 4, seed);
     const Lanes LN(threadIdx.x & 31u);
@@ -217,7 +219,8 @@ int main() {
     const int IQ = 400, IS = 2000;
     const double qe = run("core_enc", k_core_enc<true>, 1024, LDS_ENC_BYTES, IQ);
     const double q0 = run("core_enc0", k_core_enc<false>, 1024, LDS_ENC_BYTES, IQ);
-    const double qd = run("core_dec", k_core_dec, 768, LDS_DEC_BYTES, IQ);
+    const double qd = run("core_dec", k_core_dec<768>, 768, LDS_DEC_BYTES, IQ);
+    run("core_dec", k_core_dec<1024>, 1024, LDS_DEC_BYTES, IQ);
     const double cs = run("core_sha", k_core_sha, 1024, LDS_ENC_BYTES, IS);
     printf("per c2 wave-packet (64 x 500 B): encrypt core %.0f SIMD-cycles (q0 + 7 q + 3 sha), "
            "decrypt core %.0f (8 q + 2 sha)\n", q0 + 7 * qe + 3 * cs, 8 * qd + 2 * cs);

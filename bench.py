@@ -116,6 +116,33 @@ def cpu_baseline(seconds, workers, L):
     }
 
 
+def cpu_openssl(seconds, threads, L):
+    """BASELINE.md §5 item 5, the optional "strong CPU" row: the same token on
+    OpenSSL libcrypto (AES-NI / SHA-NI, key schedule and HMAC pads once per
+    key) over the host cores (tools/cpu_openssl.c, pinned to the golden
+    vectors by tests/test_cpu_openssl.py).  Not the reference path."""
+    lib_path = os.path.join(ROOT, "tools", "libcpu_openssl.so")
+    if seconds <= 0 or not os.path.exists(lib_path):
+        return None
+    import ctypes
+    lib = ctypes.CDLL(lib_path)
+    lib.cpu_openssl_run.restype = ctypes.c_double
+    lib.cpu_openssl_run.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
+    if threads <= 0:
+        threads = host_cpus()
+    done = ctypes.c_uint64()
+    t0 = time.perf_counter()
+    rate = lib.cpu_openssl_run(threads, seconds, L, ctypes.byref(done))
+    wall = time.perf_counter() - t0
+    if rate <= 0:
+        return {"error": "OpenSSL round trip failed"}
+    return {"value": rate, "unit": "round trips/s (packets encrypted then decrypted)", "gib_s": rate * L / 2**30,
+            "cores": threads, "kind": "openssl (not the reference path)",
+            "sample": f"{done.value} round trips of {L} B packets, one key per thread, OpenSSL libcrypto "
+                      f"EVP aes-256-cbc + SHA-256 HMAC with hoisted pads, {threads} threads for ~{seconds:.0f} s; "
+                      f"wall {wall:.1f} s"}
+
+
 def host_cpus():
     """The CPUs this process can actually use: its affinity mask, capped by
     the cgroup CPU quota when one is set (cgroup v2 cpu.max, v1
@@ -277,6 +304,8 @@ def main():
     hbm_bytes = bytes_dec if dom == "decrypt" else bytes_enc
 
     cpu = cpu_baseline(args.cpu_seconds, args.cpu_workers, L) if world == 1 and rank == 0 else None
+    cpu_ssl = (cpu_openssl(min(args.cpu_seconds, 5.0), args.cpu_workers, L)
+               if world == 1 and rank == 0 else None)
     pkts_total = n * world * args.steps
     value = pkts_total / elapsed
     line = {
@@ -335,6 +364,7 @@ def main():
                              "v_add3 and SGPR-operand ops 4.24 cycles, full-rate 2.40, each LDS lookup ~1.7 SIMD-cycles of "
                              "the waves beside it; LDS and VALU work overlap, DESIGN.md §4.5)"},
         "cpu_baseline": cpu,
+        "cpu_openssl": cpu_ssl,
         "e2e_pcie": e2e,
         "sharded_c4": None,
     }

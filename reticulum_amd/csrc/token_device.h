@@ -391,7 +391,6 @@ __device__ __forceinline__ void dec_quad(u32x4 p[4], const u32x4 c[4], u32x4 cha
     for (int b = 0; b < 4; ++b) {
         s[b][0] = c[b].x ^ dk[0]; s[b][1] = c[b].y ^ dk[1]; s[b][2] = c[b].z ^ dk[2]; s[b][3] = c[b].w ^ dk[3];
     }
-#ifndef RNSTOK_DEC_WIDE
 #pragma unroll
     for (int r = 1; r < NR; ++r) {
 #pragma unroll
@@ -406,23 +405,6 @@ __device__ __forceinline__ void dec_quad(u32x4 p[4], const u32x4 c[4], u32x4 cha
             tround_mix(s[b], v, dk + 4 * r);
         }
     }
-#else
-    // all four blocks' lookups in flight (64 values) around four SHA rounds
-#pragma unroll
-    for (int r = 1; r < NR; ++r) {
-        uint32_t v[4][16];
-#pragma unroll
-        for (int b = 0; b < 4; ++b) tround_load<true>(v[b], s[b], L);
-        if (WITH_SHA) {
-            RT_FENCE();
-#pragma unroll
-            for (int b = 0; b < 4; ++b) S.round((r - 1) * 4 + b);
-            RT_FENCE();
-        }
-#pragma unroll
-        for (int b = 0; b < 4; ++b) tround_mix(s[b], v[b], dk + 4 * r);
-    }
-#endif
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
         u32x4 o;

@@ -124,22 +124,12 @@ struct Keys {
                 rk[4 * i] = v.x; rk[4 * i + 1] = v.y; rk[4 * i + 2] = v.z; rk[4 * i + 3] = v.w;
             }
         } else {
-#ifdef RNSTOK_KEYS_VGPR
-            // one key, schedule in VGPRs: a VALU op with an SGPR operand issues
-            // at half rate on gfx950 (tools/cost_probe.hip)
-#pragma unroll
-            for (int i = 0; i < NR + 1; ++i) {
-                u32x4 v = *(const u32x4 *)(rec + base + 4 * i);
-                rk[4 * i] = v.x; rk[4 * i + 1] = v.y; rk[4 * i + 2] = v.z; rk[4 * i + 3] = v.w;
-            }
-#pragma unroll
-            for (int i = 0; i < 4 * (NR + 1); ++i) asm volatile("" : "+v"(rk[i]));
-#else
             // one key for the whole launch: keep the schedule in SGPRs (VOP3
-            // operands), leaving the VGPR budget to the AES/SHA chains
+            // operands), leaving the VGPR budget to the AES/SHA chains (a VALU
+            // op with an SGPR operand issues at half rate, but the schedule in
+            // VGPRs, whole or in part, measured slower: DESIGN.md §4.5)
 #pragma unroll
             for (int i = 0; i < 4 * (NR + 1); ++i) rk[i] = __builtin_amdgcn_readfirstlane(rec[base + i]);
-#endif
         }
     }
 };
@@ -203,9 +193,6 @@ template <int NR, bool PERKEY>
 __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encrypt(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
     fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);
-#ifdef RNSTOK_SETPRIO
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= blockDim.x / 2) __builtin_amdgcn_s_setprio(1);
-#endif
     const Lanes LN(threadIdx.x & 31u);
 
     Keys<NR, PERKEY> K;
@@ -647,9 +634,6 @@ template <int NR, bool PERKEY, int WG = PERKEY ? WG_PERKEY_DEC : WG_DEC>
 __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
     fill_tables<true>(tab_u32, a.sbox, a.sbox + 256);
-#ifdef RNSTOK_SETPRIO
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= blockDim.x / 2) __builtin_amdgcn_s_setprio(1);
-#endif
     const Lanes LN(threadIdx.x & 31u);
 
     Keys<NR, PERKEY> K;

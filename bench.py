@@ -329,11 +329,11 @@ def main():
                    "row_strides": {"plaintext": ps, "token": ts},
                    "step": "encrypt+MAC then verify+decrypt of the same batch", "parallelism": f"shard{world}"},
         "kernels": {
-            "encrypt": {"ms": enc_avg, "packets_s": n / (enc_avg * 1e-3),
+            "encrypt": {"ms": enc_avg, "ms_median": enc_ms[len(enc_ms) // 2], "packets_s": n / (enc_avg * 1e-3),
                         "gib_s": n * L / (enc_avg * 1e-3) / 2**30,
                         "valu_frac": ops_e / (enc_avg * 1e-3) / peak_valu,
                         "lds_frac": n * blocks(L) * LDS_LOOKUPS_PER_BLOCK / (enc_avg * 1e-3) / peak_lds},
-            "decrypt": {"ms": dec_avg, "packets_s": n / (dec_avg * 1e-3),
+            "decrypt": {"ms": dec_avg, "ms_median": dec_ms[len(dec_ms) // 2], "packets_s": n / (dec_avg * 1e-3),
                         "gib_s": n * L / (dec_avg * 1e-3) / 2**30,
                         "valu_frac": ops_d / (dec_avg * 1e-3) / peak_valu,
                         "lds_frac": n * blocks(L) * LDS_LOOKUPS_PER_BLOCK / (dec_avg * 1e-3) / peak_lds},

@@ -643,7 +643,13 @@ def issue_model(kernel, n, L, keys, n_cu, ms, clock_ghz):
 
 def _newest_pmc(kernel, n, L, keys):
     import glob
-    for path in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))):
+    import re
+
+    def order(path):   # r02y < r02aa < r02ak: round, then tag length, then tag
+        m = re.match(r"r(\d+)([a-z]+)_pmc\.json$", os.path.basename(path))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=order, reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)

@@ -117,6 +117,13 @@ static void *worker(void *arg) {
     const int L = j->L, T = 16 + 16 * (L / 16 + 1) + 32;
     uint8_t key[64], iv[16];
     uint8_t *pt = malloc((size_t)RING * (L + 1)), *tok = malloc((size_t)T), *back = malloc((size_t)T);
+    if (!pt || !tok || !back) {
+        free(pt);
+        free(tok);
+        free(back);
+        j->ok = 0;
+        return NULL;
+    }
     uint32_t s = 0x9E3779B9u * (uint32_t)(j->seed + 1);
 #define RND() (s ^= s << 13, s ^= s >> 17, s ^= s << 5, (uint8_t)s)
     for (int i = 0; i < 64; ++i) key[i] = RND();
@@ -152,6 +159,11 @@ static void *worker(void *arg) {
 double cpu_openssl_run(int threads, double seconds, int L, uint64_t *packets_out) {
     pthread_t *th = calloc((size_t)threads, sizeof(pthread_t));
     Job *jobs = calloc((size_t)threads, sizeof(Job));
+    if (!th || !jobs || threads <= 0) {
+        free(th);
+        free(jobs);
+        return -1.0;
+    }
     double rate = 0;
     uint64_t total = 0;
     int ok = 1;
@@ -159,10 +171,13 @@ double cpu_openssl_run(int threads, double seconds, int L, uint64_t *packets_out
         jobs[i].seconds = seconds;
         jobs[i].L = L;
         jobs[i].seed = i;
-        pthread_create(&th[i], NULL, worker, &jobs[i]);
+        if (pthread_create(&th[i], NULL, worker, &jobs[i])) {   // run it here instead
+            worker(&jobs[i]);
+            th[i] = 0;
+        }
     }
     for (int i = 0; i < threads; ++i) {
-        pthread_join(th[i], NULL);
+        if (th[i]) pthread_join(th[i], NULL);
         ok &= jobs[i].ok;
         total += jobs[i].packets;
         if (jobs[i].busy > 0) rate += jobs[i].packets / jobs[i].busy;

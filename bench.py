@@ -362,7 +362,9 @@ def main():
                              "traffic_detail.calibration). issue_model = the kernel's own instruction mix priced with the "
                              "per-instruction issue costs measured by tools/cost_probe.hip (half-rate v_perm/v_alignbit/"
                              "v_add3 and SGPR-operand ops 4.24 cycles, full-rate 2.40, each LDS lookup ~1.7 SIMD-cycles of "
-                             "the waves beside it; LDS and VALU work overlap, DESIGN.md §4.5)"},
+                             "the waves beside it; LDS and VALU work overlap, DESIGN.md §4.5); issue_model.measured_core = the "
+                             "same composition with each piece timed (the kernel's own compute core from registers, "
+                             "tools/floor_probe.hip) instead of priced"},
         "cpu_baseline": cpu,
         "cpu_openssl": cpu_ssl,
         "e2e_pcie": e2e,
@@ -627,6 +629,15 @@ ISSUE_CYCLES_PER_WAVE_PACKET_500B = {
     # 8 quads (AES + SHA of the same quad) + 2 finishing compressions
     "decrypt": 8 * (10057 + 1523) + 2 * 4798,
 }
+# The same per-wave-packet composition measured instead of priced: the
+# kernels' own enc_quad / dec_quad / sha256_compress in register-only loops
+# at c2's launch shape (tools/floor_probe.hip, profiles/r02af_floor_probe.txt;
+# SIMD-cycles per wave-iteration: enc quad 12 583, quad 0 8 381, dec quad at
+# 768 threads 13 437, compression 5 306).
+CORE_CYCLES_PER_WAVE_PACKET_500B = {
+    "encrypt": 8381 + 7 * 12583 + 3 * 5306,
+    "decrypt": 8 * 13437 + 2 * 5306,
+}
 
 
 def issue_model(kernel, n, L, keys, n_cu, ms, clock_ghz):
@@ -636,9 +647,14 @@ def issue_model(kernel, n, L, keys, n_cu, ms, clock_ghz):
     waves_per_simd = n / 64 / (n_cu * 4)
     cycles = ISSUE_CYCLES_PER_WAVE_PACKET_500B[kernel] * waves_per_simd
     floor_ms = cycles / (clock_ghz * 1e9) * 1e3
+    core = CORE_CYCLES_PER_WAVE_PACKET_500B[kernel] * waves_per_simd
+    core_ms = core / (clock_ghz * 1e9) * 1e3
     return {"floor_cycles_per_simd": cycles, "clock_ghz": clock_ghz, "floor_ms": floor_ms,
             "frac_of_issue_floor": floor_ms / ms,
-            "floor_ms_at_2p4ghz": cycles / 2.4e9 * 1e3}
+            "floor_ms_at_2p4ghz": cycles / 2.4e9 * 1e3,
+            "measured_core": {"cycles_per_simd": core, "ms": core_ms, "frac": core_ms / ms,
+                              "source": "tools/floor_probe.hip (the kernel's own quad/compression code from "
+                                        "registers only, no memory or packet loop), profiles/r02af_floor_probe.txt"}}
 
 
 def _newest_pmc(kernel, n, L, keys):

@@ -43,3 +43,34 @@ def test_guard_finish_cancels():
              "time.sleep(1.0)\n"
              "print('done')\n")
     assert p.returncode == 0 and p.stdout.strip() == "done"
+
+
+def test_roofline_models_and_newest_profile():
+    """The issue model and the measured compute core of the c2 kernels, and
+    the choice of the newest committed PMC run by round tag (r02y < r02aa)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    m = bench.issue_model("encrypt", 1 << 20, 500, 1, 256, 1.0, 2.0)
+    assert m["measured_core"]["cycles_per_simd"] > m["floor_cycles_per_simd"] > 0
+    assert abs(m["measured_core"]["frac"] - m["measured_core"]["ms"] / 1.0) < 1e-12
+    assert bench.issue_model("encrypt", 1 << 20, 100, 1, 256, 1.0, 2.0) is None   # c2 shape only
+    path, d = bench._newest_pmc("encrypt", 1 << 20, 500, 1)
+    assert path is not None and "encrypt" in d
+    import glob
+    import re
+    cands = []
+    for p in glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")):
+        t = re.match(r"r(\d+)([a-z]+)_pmc\.json$", os.path.basename(p))
+        with open(p) as f:
+            w = json.load(f).get("_workload", {})
+        if t and (w.get("packets"), w.get("length"), w.get("keys")) == (1 << 20, 500, 1):
+            cands.append(((int(t.group(1)), len(t.group(2)), t.group(2)), p))
+    assert path == max(cands)[1]
+
+
+def test_cpu_openssl_row_without_library(tmp_path, monkeypatch):
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))     # no tools/libcpu_openssl.so there
+    assert bench.cpu_openssl(1.0, 1, 500) is None
+    assert bench.cpu_openssl(0.0, 1, 500) is None

@@ -16,6 +16,9 @@
 //   core_dec   : dec_quad<14, true> (4 independent blocks + one compression),
 //                at 768 threads (the c2 kernel's shape) and at 1024
 //   core_sha   : sha256_compress alone (hmac_finish's compressions)
+//   core_enc_x2: two packets per lane (two CBC chains and two compressions
+//                interleaved round by round) at 512 threads = 2 waves/SIMD,
+//                round keys in SGPRs or (x2vk) in VGPRs
 //
 // Per c2 wave-packet (64 packets of 500 B): encrypt = 1 x core_enc0 + 7 x
 // core_enc + 3 x core_sha; decrypt = 8 x core_dec + 2 x core_sha.  The host
@@ -102,6 +105,102 @@ __global__ __launch_bounds__(1024) void k_core_enc(const uint32_t *rec, uint32_t
     uint32_t acc = prev.x ^ prev.y ^ prev.z ^ prev.w;
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc ^= h[k];
+    STAMP_END(acc)
+}
+
+// Two packets per lane, their CBC chains and SHA rounds interleaved round by
+// round (ILP inside the wave instead of across waves), at 2 waves/SIMD; the
+// round keys in SGPRs (VK = false) or in VGPRs (VK = true: 256 VGPRs allow it).
+template <int NR, bool VK>
+__device__ __forceinline__ void enc_quad_x2(u32x4 c[2][4], const u32x4 x[2][4], const u32x4 chain[2],
+                                            const uint32_t *rk, const Lanes &L, Sha256 S[2]) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        uint32_t st[2][4];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const u32x4 in = x[k][b] ^ (b == 0 ? chain[k] : c[k][b - 1]);
+            st[k][0] = in.x ^ rk[0]; st[k][1] = in.y ^ rk[1]; st[k][2] = in.z ^ rk[2]; st[k][3] = in.w ^ rk[3];
+        }
+#pragma unroll
+        for (int r = 1; r < NR; ++r) {
+            uint32_t v[2][16];
+            tround_load<false>(v[0], st[0], L);
+            tround_load<false>(v[1], st[1], L);
+            S[0].round(b * NR + r - 1);
+            S[1].round(b * NR + r - 1);
+            tround_mix(st[0], v[0], rk + 4 * r);
+            tround_mix(st[1], v[1], rk + 4 * r);
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t s0 = st[k][0], s1 = st[k][1], s2 = st[k][2], s3 = st[k][3];
+            c[k][b].x = tlast_enc(s0, s1, s2, s3, rk[4 * NR + 0], L);
+            c[k][b].y = tlast_enc(s1, s2, s3, s0, rk[4 * NR + 1], L);
+            c[k][b].z = tlast_enc(s2, s3, s0, s1, rk[4 * NR + 2], L);
+            c[k][b].w = tlast_enc(s3, s0, s1, s2, rk[4 * NR + 3], L);
+            S[k].round(b * NR + NR - 1);
+        }
+    }
+#pragma unroll
+    for (int i = 4 * NR; i < 64; ++i) {
+        S[0].round(i);
+        S[1].round(i);
+    }
+}
+
+template <bool VK>
+__global__ __launch_bounds__(512) void k_core_enc_x2(const uint32_t *rec, uint32_t *out, Stamp *st, uint32_t seed, int iters) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
+    fill_any(tab, LDS_ENC_BYTES / 4, seed);
+    const Lanes LN(threadIdx.x & 31u);
+    uint32_t rk[60];
+#pragma unroll
+    for (int i = 0; i < 60; ++i) rk[i] = __builtin_amdgcn_readfirstlane(rec[i]);
+    if (VK) {
+#pragma unroll
+        for (int i = 0; i < 60; ++i) asm volatile("" : "+v"(rk[i]));
+    }
+    const uint32_t t = threadIdx.x * 0x9E3779B9u ^ seed;
+    u32x4 x[2][4], c[2][4], prev[2];
+    Sha256 S[2];
+    uint32_t h[2][8];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t tk = t + 0x1234567u * k;
+        prev[k] = u32x4{tk, tk + 1, tk + 2, tk + 3};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[k][j] = u32x4{tk ^ j, tk + 7 * j, tk * 3 + j, tk ^ (j << 9)};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) S[k].w[i] = tk + i;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) h[k][i] = rk[i] ^ tk;
+    }
+    STAMP_BEGIN()
+#pragma nounroll
+    for (int i = 0; i < iters; ++i) {
+        S[0].start(h[0]);
+        S[1].start(h[1]);
+        enc_quad_x2<14, VK>(c, x, prev, rk, LN, S);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(S[k].v[j]));
+#pragma unroll
+            for (int j = 0; j < 8; ++j) h[k][j] += S[k].v[j];
+            sha_units(S[k].w, prev[k], c[k][0], c[k][1], c[k][2]);
+            prev[k] = c[k][3];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[k][j] = c[k][j] ^ x[k][j];
+        }
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        acc ^= prev[k].x ^ prev[k].w;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc ^= h[k][j];
+    }
     STAMP_END(acc)
 }
 
@@ -222,6 +321,11 @@ int main() {
     const double qd = run("core_dec", k_core_dec<768>, 768, LDS_DEC_BYTES, IQ);
     run("core_dec", k_core_dec<1024>, 1024, LDS_DEC_BYTES, IQ);
     const double cs = run("core_sha", k_core_sha, 1024, LDS_ENC_BYTES, IS);
+    // 2 packets per lane at 2 waves/SIMD: per-packet cost = cycles per wave-iteration / 2
+    const double x2s = run("core_enc_x2", k_core_enc_x2<false>, 512, LDS_ENC_BYTES, IQ);
+    const double x2v = run("core_enc_x2vk", k_core_enc_x2<true>, 512, LDS_ENC_BYTES, IQ);
+    printf("two packets per lane: %.0f (SGPR keys) / %.0f (VGPR keys) SIMD-cycles per packet-quad, against %.0f\n",
+           x2s / 2, x2v / 2, qe);
     printf("per c2 wave-packet (64 x 500 B): encrypt core %.0f SIMD-cycles (q0 + 7 q + 3 sha), "
            "decrypt core %.0f (8 q + 2 sha)\n", q0 + 7 * qe + 3 * cs, 8 * qd + 2 * cs);
     printf("per SIMD per c2 launch (2^20 packets, %d CUs): encrypt core %.3f M cycles, decrypt core %.3f M cycles\n",

@@ -62,7 +62,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=3, help="minimum untimed warmup steps")
+    ap.add_argument("--warmup-seconds", type=float, default=0.3,
+                    help="keep warming up until this much back-to-back work has run (clock ramp)")
     ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
     ap.add_argument("--length", type=int, default=500, help="plaintext bytes per packet")
     ap.add_argument("--keys", type=int, default=1, help="1 = single link key (c2); 65536 = c3")
@@ -78,6 +80,27 @@ def parse():
     ap.add_argument("--e2e", action="store_true", default=True, help="also time the PCIe-inclusive path")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false")
     return ap.parse_args()
+
+
+def warmup(step, stream, min_steps, min_seconds):
+    """At least `min_steps` untimed steps, continued until `min_seconds` of
+    back-to-back work have run: after an idle spell the GPU's clocks ramp up
+    over ~25 steps (~50 ms) of this load, c2 steps falling from 2.0-2.45 ms to
+    a steady 1.75 ms (tools/steps_probe.py, profiles/r02ao_steps_probe.txt).
+    At most 8 steps are queued ahead of the GPU, which never idles in between."""
+    import torch
+    t0, n, prev = time.perf_counter(), 0, None
+    while n < min_steps or time.perf_counter() - t0 < min_seconds:
+        for _ in range(4):
+            step()
+        n += 4
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        if prev is not None:
+            prev.synchronize()
+        prev = ev
+    torch.cuda.synchronize()
+    return n, time.perf_counter() - t0
 
 
 def cpu_baseline(seconds, workers, L):
@@ -255,15 +278,18 @@ def main():
         if ev is not None:
             ev[2].record(stream)
 
-    for _ in range(args.warmup):
-        step()
+    # correctness gate on the benchmarked data (size-independent properties),
+    # before the warmup so that nothing idles the GPU between warmup and timing
+    step()
     torch.cuda.synchronize()
-    # correctness gate on the benchmarked data (size-independent properties)
     ok = bool((status == 0).all()) and bool((out_len == L).all()) and torch.equal(back[:, :L], pt)
     if not ok:
         raise SystemExit("bench: round trip failed on the benchmark batch")
 
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    warm_steps, warm_s = warmup(step, stream, args.warmup, args.warmup_seconds)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -316,6 +342,9 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "warmup_run": {"steps": warm_steps, "seconds": warm_s,
+                       "note": "untimed steps actually run before the timed region: at least --warmup, continued "
+                               "until --warmup-seconds of back-to-back work (GPU clock ramp-up, bench.warmup)"},
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",

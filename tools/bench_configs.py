@@ -34,6 +34,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def warm(fn, seconds=0.3):
+    """Steady clocks before timing: `fn` back to back for `seconds` (the GPU's
+    clocks ramp up over ~50 ms of work after an idle spell, bench.warmup)."""
+    import torch
+    import bench
+    bench.warmup(fn, torch.cuda.current_stream(), 2, seconds)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c5")
@@ -78,6 +86,7 @@ def main():
         okm = torch.empty((n, 64), dtype=torch.uint8, device=dev)
         e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
         hk, dk = [], []
+        warm(lambda: (device.hkdf(ikm, okm, salt), device.derive_keyset(ikm, salt)))
         for _ in range(5):
             e0.record()
             device.hkdf(ikm, okm, salt)
@@ -166,8 +175,15 @@ def main():
         bytes_pt = int(lens.sum())
         n_enc, n_dec = len(e_idx), len(d_idx)
         def check():
-            emask = torch.repeat_interleave(is_enc.to(torch.uint8), tl.to(torch.int64)).bool()
-            ok = torch.equal(tok_e[emask], tok[emask]) and not bool(tok_e[~emask].any())
+            # byte mask of the encrypt half's tokens (2.2 G bytes: repeat_interleave
+            # and mask indexing past 2^31 elements fail on ROCm, so marks + cumsum)
+            marks = torch.zeros(tok.numel() + 1, dtype=torch.int32, device=dev)
+            e_off = tok_off[e_idx]
+            marks.index_add_(0, e_off, torch.ones_like(e_off, dtype=torch.int32))
+            marks.index_add_(0, e_off + tl[e_idx].to(torch.int64), -torch.ones_like(e_off, dtype=torch.int32))
+            emask = torch.cumsum(marks, 0, dtype=torch.int32)[:-1] > 0
+            # elementwise, no boolean-mask compaction (> 2^31 elements)
+            ok = torch.equal(tok_e, torch.where(emask, tok, torch.zeros((), dtype=tok.dtype, device=dev)))
             ok = ok and bool((st[: len(d_idx)] == 0).all()) and torch.equal(ol[: len(d_idx)], lens[d_idx])
             for j in range(0, len(d_idx), 4099):
                 i = int(d_idx[j])
@@ -191,6 +207,7 @@ def main():
         dec()
     torch.cuda.synchronize()
     ok = check()
+    warm(lambda: (enc(), dec()))
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     t0 = time.perf_counter()
     for e in ev:
@@ -249,8 +266,7 @@ def ratchet_config(dev, g, steps):
 
     times = {}
     for name, fn in (("verify_trials", trial), ("decrypt_opened", opened)):
-        for _ in range(2):
-            fn()
+        warm(fn)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
         for a, b in ev:
             a.record()
@@ -287,8 +303,7 @@ def resource_config(dev, g, steps):
     first = torch.empty(n_res, dtype=torch.int32, device=dev)
     times = {}
     for name, gd in (("map_hashes", 0), ("map_hashes+collision_guard", guard)):
-        for _ in range(2):
-            device.map_hashes(data, out, salts, off, ln, res, sdu=sdu, guard=gd, first_collision=first)
+        warm(lambda: device.map_hashes(data, out, salts, off, ln, res, sdu=sdu, guard=gd, first_collision=first))
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
         for a, b in ev:
             a.record()
@@ -364,6 +379,7 @@ def wire_config(dev, g, steps):
     res = {"config": "wire", "packets": n, "packet_bytes": L, "ifac_size": isz,
            "ok": bool(ok_frames and ok_ifac and ok_unpack), "stages": {}}
     for name, (f, nbytes) in stages.items():
+        warm(f)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
         for a, b in ev:
             a.record()

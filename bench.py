@@ -478,7 +478,19 @@ def sharded_bench(cfg, args, world, rank, local, reps=3):
         n_keys = 65536
         lens = torch.randint(64, 4097, (n,), dtype=torch.int32, generator=kg)
     keys = torch.randint(0, 256, (n_keys, 64), dtype=torch.uint8, generator=kg).numpy()
-    ks = rt.KeySet(keys if n_keys > 1 else keys[0].tobytes(), device=local)
+    keys_ms = None
+    if dist_on and world > 1:
+        # rank 0 holds the key table; every rank receives it over RCCL and
+        # expands its own copy on its GPU
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        ks = shard.broadcast_keyset(torch.from_numpy(keys).to(dev) if rank == 0 else None, src=0, device=dev)
+        torch.cuda.synchronize()
+        dist.barrier()
+        keys_ms = (time.perf_counter() - t0) * 1e3
+    else:
+        ks = rt.KeySet(keys if n_keys > 1 else keys[0].tobytes(), device=local)
     uniform = cfg == "c4"
 
     def offsets(lengths):
@@ -626,7 +638,7 @@ def sharded_bench(cfg, args, world, rank, local, reps=3):
         "gib_s": byts_all / total["compute_s"] / 2**30,
         "end_to_end_packets_s": pkts / (total["scatter_s"] + total["compute_s"] + total["gather_s"]),
         "scatter_ms": total["scatter_s"] * 1e3, "compute_ms": total["compute_s"] * 1e3,
-        "gather_ms": total["gather_s"] * 1e3, "scaling": "strong", "ok": ok,
+        "gather_ms": total["gather_s"] * 1e3, "key_broadcast_setup_ms": keys_ms, "scaling": "strong", "ok": ok,
         "data": "synthetic random plaintext, IVs and keys generated on rank 0's device",
     })
     report["config"] = {

@@ -203,6 +203,23 @@ def hkdf(ikm, out, salt=None, context=None, stream=None):
                               length, n, _stream(stream)))
 
 
+def keyset(keys, stream=None):
+    """KeySet from a device key table (Token.py:58-74 per row): ``keys`` is a
+    contiguous (n_keys, 64 or 32) uint8 CUDA tensor, e.g. received by
+    shard.broadcast_keys; expanded on its device on ``stream`` without a
+    host round trip.  Usable from any stream right away, as derive_keyset."""
+    _check_u8(keys)
+    if keys.dim() != 2 or keys.shape[1] not in (32, 64) or keys.shape[0] < 1 or not keys.is_contiguous():
+        raise ValueError("keys must be a contiguous (n_keys, 64 or 32) uint8 device tensor")
+    n, klen = keys.shape
+    lib = _native.load()
+    ctx = _native.context(keys.device.index)
+    h = lib.rt_keyset_create_device(ctx, _p(keys), klen, n, _stream(stream))
+    if not h:
+        raise _native.NativeError(-1, _native.last_error())
+    return KeySet._adopt(h, klen, n, lib, ctx)
+
+
 def derive_keyset(ikm, salt=None, context=None, key_len=64, stream=None):
     """Per-packet keying from device rows (Identity.py:837-846): KeySet whose
     key i is Token(hkdf(key_len, ikm[i], salt[i], context)); derived and

@@ -100,6 +100,39 @@ def _default_device(group):
     return torch.device("cpu")
 
 
+def broadcast_keys(keys, src=0, group=None, device=None):
+    """The key table (n_keys, 64 or 32) uint8 held on ``src`` (ignored, may be
+    None, elsewhere), on every rank (per-packet key tables are
+    broadcast, each rank expands its own copy; 65 536 x 64 B = 4 MiB, one
+    RCCL broadcast over xGMI).  Returns the contiguous table on ``device``."""
+    rank = dist.get_rank(group)
+    dev = device if device is not None else (keys.device if keys is not None else _default_device(group))
+    if rank == src:
+        k = torch.as_tensor(keys)
+        if k.dtype != torch.uint8 or k.dim() != 2 or k.shape[1] not in (32, 64) or k.shape[0] < 1:
+            raise ValueError("keys must be a (n_keys, 64 or 32) uint8 table")
+        shape = torch.tensor([k.shape[0], k.shape[1]], dtype=torch.int64, device=dev)
+    else:
+        shape = torch.empty(2, dtype=torch.int64, device=dev)
+    dist.broadcast(shape, src, group=group)
+    n, klen = (int(x) for x in shape)
+    out = k.contiguous().to(dev) if rank == src else torch.empty((n, klen), dtype=torch.uint8, device=dev)
+    if _staged(group) and out.is_cuda:          # gloo: through a host copy
+        h = out.cpu()
+        dist.broadcast(h, src, group=group)
+        out.copy_(h)
+    else:
+        dist.broadcast(out, src, group=group)
+    return out
+
+
+def broadcast_keyset(keys, src=0, group=None, device=None, stream=None):
+    """broadcast_keys, then a device KeySet of the table on every rank
+    (device.keyset: expanded on the GPU, no host round trip)."""
+    from . import device as _device
+    return _device.keyset(broadcast_keys(keys, src, group, device), stream=stream)
+
+
 def scatter_packed(buf, off, length, bounds, src=0, group=None, device=None, rows=()):
     """Send each rank its packet range of a packed batch held on ``src``.
 

@@ -395,3 +395,34 @@ def test_config_c5_full_size(rt):
         assert s == int(sth[i - h]), i
         if s == 0:
             assert hback[coff[i]:coff[i] + lens[i]].tobytes() == p, i
+
+
+# ------------------------------------------------ key table from device memory
+
+@pytest.mark.parametrize("klen", [64, 32])
+def test_device_keyset_from_table(rt, klen):
+    """device.keyset (the per-rank step after shard.broadcast_keys): a key
+    table already in HBM expanded on the device; used at once from the device
+    path and from the host path, every token bit-exact vs the oracle."""
+    import torch
+    from reticulum_amd import device
+    rng = np.random.Generator(np.random.PCG64(41 + klen))
+    nk, n, L = 300, 2000, 77
+    keys = rng.integers(0, 256, (nk, klen), dtype=np.uint8)
+    ks = device.keyset(torch.from_numpy(keys).cuda())
+    assert (ks.n_keys, ks.key_len) == (nk, klen)
+    kidx = rng.integers(0, nk, n).astype(np.int32)
+    pt = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    iv = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    tl = rt.token_len(L)
+    tok = torch.empty((n, tl), dtype=torch.uint8, device="cuda")
+    device.encrypt_uniform(ks, torch.from_numpy(pt).cuda(), L, torch.from_numpy(iv).cuda(), tok,
+                           key_idx=torch.from_numpy(kidx).cuda())
+    torch.cuda.synchronize()
+    t = tok.cpu().numpy()
+    for i in range(0, n, 97):
+        assert t[i].tobytes() == oracle.encrypt(keys[kidx[i]].tobytes(), iv[i].tobytes(), pt[i].tobytes())
+    back, status = ks.decrypt_batch([t[i].tobytes() for i in range(n)], key_idx=kidx)
+    assert (status == 0).all() and back.to_list() == [pt[i].tobytes() for i in range(n)]
+    with pytest.raises(ValueError):
+        device.keyset(torch.zeros((4, 48), dtype=torch.uint8, device="cuda"))

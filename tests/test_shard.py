@@ -176,3 +176,57 @@ def test_slice_handles_unordered_offsets():
     assert l.dtype == torch.int32 and o.dtype == torch.int64
     for i in range(3):
         assert b[int(o[i]):int(o[i]) + int(l[i])].tolist() == buf[int(off[i]):int(off[i]) + int(ln[i])].tolist()
+
+
+def _keys_worker(rank, world, port, result_q):
+    import torch.distributed as dist
+    from oracle import ctoken
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    table = torch.from_numpy(np.random.Generator(np.random.PCG64(9)).integers(0, 256, (1000, 64), dtype=np.uint8))
+    got = shard.broadcast_keys(table if rank == 0 else None, src=0)
+    # every rank holds rank 0's table and its tokens under key 999 match the oracle's
+    ok = got.dtype == torch.uint8 and tuple(got.shape) == (1000, 64) and torch.equal(got, table)
+    iv = bytes(16)
+    ok = ok and ctoken.encrypt(got[999].numpy().tobytes(), iv, b"x" * 33) == \
+        ctoken.encrypt(table[999].numpy().tobytes(), iv, b"x" * 33)
+    flags = torch.tensor([int(ok)], dtype=torch.int32)
+    dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        result_q.put(bool(flags[0]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_broadcast_keys_gloo_world2():
+    """The c3/c5 key table held by rank 0 reaches every rank (SURVEY §8(e):
+    broadcast, then a per-rank key setup; device.keyset builds that on GPUs)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_keys_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get() is True
+
+
+def test_broadcast_keys_rejects_bad_tables():
+    """A table that is not (n, 64 or 32) uint8 is refused on the source
+    before any collective runs (world size 1, gloo)."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        for bad in (torch.zeros((4, 48), dtype=torch.uint8), torch.zeros((4, 64), dtype=torch.int32),
+                    torch.zeros((0, 64), dtype=torch.uint8), torch.zeros(64, dtype=torch.uint8)):
+            with pytest.raises(ValueError):
+                shard.broadcast_keys(bad, src=0)
+        assert torch.equal(shard.broadcast_keys(torch.ones((3, 32), dtype=torch.uint8), src=0),
+                           torch.ones((3, 32), dtype=torch.uint8))
+    finally:
+        dist.destroy_process_group()

@@ -343,8 +343,14 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, const
     if (npairs > max_pairs) npairs = max_pairs;
     const uint32_t lane = threadIdx.x & 63u, rl = lane & 15u;
     const uint64_t g0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, ng = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t g = g0; 4 * g < npairs; g += ng) {
-        const uint64_t k = 4 * g + (lane >> 4);
+    // Each row takes two consecutive flag pairs: a Reticulum stream alternates
+    // frames with the empty 7E|7E gaps between them, and with one pair per
+    // row every other row idled on a gap (unescape 546 -> 459 us, A/B in
+    // profiles/r02av_unesc_pair2_ab.txt).
+    constexpr uint32_t PPR = 2;
+    for (uint64_t g = g0; 4 * PPR * g < npairs; g += ng) {
+      for (uint32_t sub = 0; sub < PPR; ++sub) {
+        const uint64_t k = 4 * PPR * g + PPR * (lane >> 4) + sub;
         const bool valid = k < npairs;
         const uint64_t a = valid ? pos[k] + 1 : 0, e = valid ? pos[k + 1] : 0;
         uint8_t *o = out + a;
@@ -401,6 +407,7 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, const
                                                ? RT_FRAME_BAD_LEN
                                                : RT_FRAME_OK);
         }
+      }
     }
 }
 

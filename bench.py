@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2 (default) / c3: weak-scaling token steps; c4 / c5: sharded batch held by rank 0")
     ap.add_argument("--sharded-reps", type=int, default=3, help="timed passes of a sharded config")
+    ap.add_argument("--sharded-chunks", type=int, default=4,
+                    help="N > 1: chunks per rank of the pipelined sharded pass (0 disables it)")
     ap.add_argument("--sharded-timeout", type=float, default=150.0,
                     help="N > 1: seconds allowed for the sharded c4 pass after the headline")
     ap.add_argument("--e2e", action="store_true", default=True, help="also time the PCIe-inclusive path")
@@ -310,10 +312,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, enc_avg, dec_avg = t.tolist()
 
-    # PCIe-inclusive (host buffers, pinned) rate for DESIGN.md; rank 0 only.
+    # PCIe-inclusive (host buffers, pinned) rate for DESIGN.md: every rank at
+    # once on its own shard, over its own PCIe link (the node's host-origin rate)
     e2e = None
-    if args.e2e and rank == 0:
-        e2e = e2e_rate(ks, pt, iv, L, tl, n, stream)
+    if args.e2e:
+        if world > 1:
+            e2e = e2e_rate(ks, pt, iv, L, tl, n, stream, sync_all=dist.barrier,
+                           reduce_max=lambda v: _reduce_max(v, dev), world=world)
+        else:
+            e2e = e2e_rate(ks, pt, iv, L, tl, n, stream)
 
     lib = _native.load()
     n_cu = lib.rt_num_cus(_native.context(local))
@@ -329,9 +336,10 @@ def main():
     bytes_dec = n * (tl + (tl - 48) + 8)      # read token, write pt + len + status
     hbm_bytes = bytes_dec if dom == "decrypt" else bytes_enc
 
-    cpu = cpu_baseline(args.cpu_seconds, args.cpu_workers, L) if world == 1 and rank == 0 else None
-    cpu_ssl = (cpu_openssl(min(args.cpu_seconds, 5.0), args.cpu_workers, L)
-               if world == 1 and rank == 0 else None)
+    # the CPU baselines run on rank 0 at N = 1 here; at N > 1 after the sharded
+    # pass, while the other ranks wait idle (below)
+    cpu = cpu_baseline(args.cpu_seconds, args.cpu_workers, L) if world == 1 else None
+    cpu_ssl = cpu_openssl(min(args.cpu_seconds, 5.0), args.cpu_workers, L) if world == 1 else None
     pkts_total = n * world * args.steps
     value = pkts_total / elapsed
     line = {
@@ -375,25 +383,23 @@ def main():
                      "algorithmic_bytes_per_launch": hbm_bytes,
                      "algorithmic_hbm_gb_s": hbm_bytes / (dom_ms * 1e-3) / 1e9,
                      "frac_of_survey_P": achieved / (n_cu * 64 * 2.4e9),
-                     "measured_valu_peak": n_cu * 4 * 64 / 2.74 * 2.4e9 / 1e12,
-                     "frac_of_measured_valu_peak": achieved / (n_cu * 4 * 64 / 2.74 * 2.4e9),
                      "sustained_clock_ghz": sustained_clock_ghz(dom, n, L, args.keys),
                      "lds_frac": n * blocks(L) * LDS_LOOKUPS_PER_BLOCK / (dom_ms * 1e-3) / peak_lds,
                      "issue_model": issue_model(dom, n, L, args.keys, n_cu, dom_ms,
-                                                sustained_clock_ghz(dom, n, L, args.keys)),
+                                                sustained_clock_ghz(dom, n, L, args.keys),
+                                                (_newest_pmc(dom, n, L, args.keys)[1] or {}).get(dom)),
                      "note": "achieved = canonical int32 VALU lane-ops per launch (SURVEY §8(d): 352/AES block, "
                              "1464/SHA-256 compression, +8 tag compare) / HIP-event kernel time; peak = CUs x 128 "
-                             "lanes x 2.4 GHz (full-rate VALU, MI355X_MICROARCH.md); measured_valu_peak = v_xor_b32 at 2.74 cycles "
-                             "per wave64 instruction per SIMD (tools/valu_peak.hip); sustained_clock_ghz from the "
-                             "committed PMC run (GRBM_GUI_ACTIVE / 8 XCDs / kernel-trace average); frac_of_survey_P uses "
-                             "BASELINE.md §5's P = CUs x 64 x 2.4 GHz; traffic = HBM bytes per launch from the committed "
-                             "rocprofv3 PMC summary (profiles/*_pmc.json, FETCH_SIZE x 2 + WRITE_SIZE; see "
-                             "traffic_detail.calibration). issue_model = the kernel's own instruction mix priced with the "
-                             "per-instruction issue costs measured by tools/cost_probe.hip (half-rate v_perm/v_alignbit/"
-                             "v_add3 and SGPR-operand ops 4.24 cycles, full-rate 2.40, each LDS lookup ~1.7 SIMD-cycles of "
-                             "the waves beside it; LDS and VALU work overlap, DESIGN.md §4.5); issue_model.measured_core = the "
-                             "same composition with each piece timed (the kernel's own compute core from registers, "
-                             "tools/floor_probe.hip) instead of priced"},
+                             "lanes x 2.4 GHz (MI355X_MICROARCH.md), i.e. two wave64 VALU instructions per SIMD per "
+                             "4-cycle issue slot, which gfx950 reaches only by dual issue of full-rate VGPR-only ops "
+                             "from two waves (tools/issue_model_probe.hip, profiles/r03b_issue_model_probe.txt); "
+                             "sustained_clock_ghz from the committed PMC run (GRBM_GUI_ACTIVE / 8 XCDs / kernel-trace "
+                             "average); frac_of_survey_P uses BASELINE.md §5's P = CUs x 64 x 2.4 GHz; traffic = HBM "
+                             "bytes per launch from the committed rocprofv3 PMC summary (profiles/*_pmc.json, FETCH_SIZE "
+                             "x 2 + WRITE_SIZE; see traffic_detail.calibration). issue_model = the kernel's issue slots "
+                             "from its ISA (floor: every dual-issuable op paired; ceiling: none), its issued slots from "
+                             "the PMC (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2 + SQ_INSTS_LDS), and measured_core = the "
+                             "kernel's own compute core timed from registers (tools/floor_probe.hip); DESIGN.md §4.5"},
         "cpu_baseline": cpu,
         "cpu_openssl": cpu_ssl,
         "e2e_pcie": e2e,
@@ -417,10 +423,56 @@ def main():
         guard.finish()
     elif world > 1:
         dist.barrier()
+    if world > 1:
+        # north_star: the reference path timed on the same box's host cores in
+        # the same run, at every N.  Rank 0 runs it after the GPU work; the
+        # other ranks block on the rendezvous store (a socket read, no spinning
+        # host thread competing for the cores being timed).
+        _cpu_phase(line, args, L, rank)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _reduce_max(values, dev):
+    """Elementwise max of a list of floats over all ranks."""
+    import torch
+    import torch.distributed as dist
+    on = dev if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor(values, dtype=torch.float64, device=on)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.tolist()
+
+
+def _cpu_phase(line, args, L, rank):
+    """N > 1: cpu_baseline and cpu_openssl on rank 0; the other ranks wait on
+    the process group's store until rank 0 is done (dist.barrier instead when
+    the store is not reachable)."""
+    import torch.distributed as dist
+    store = None
+    try:
+        store = dist.distributed_c10d._get_default_store()
+    except Exception:   # noqa: BLE001 (private API; fall back to a barrier)
+        store = None
+    key = "rnstok_bench_cpu_done"
+    if rank == 0:
+        try:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_workers, L)
+            line["cpu_openssl"] = cpu_openssl(min(args.cpu_seconds, 5.0), args.cpu_workers, L)
+        except Exception as e:  # reported, never fatal for the headline line
+            line["cpu_baseline"] = {"error": f"{type(e).__name__}: {e}"}
+        if line.get("cpu_baseline") and "error" not in line["cpu_baseline"]:
+            line["cpu_baseline"]["note"] = ("timed on rank 0 after the GPU phases of this N > 1 run, the other "
+                                            "ranks idle (blocked on the rendezvous store)")
+        if store is not None:
+            store.set(key, "1")
+    if store is not None:
+        if rank != 0:
+            import datetime
+            store.wait([key], datetime.timedelta(seconds=max(120.0, 4 * args.cpu_seconds + 60)))
+    else:
+        dist.barrier()
 
 
 class _LineGuard:
@@ -468,13 +520,17 @@ def sharded_bench(cfg, args, world, rank, local, reps=3):
     dist_on = dist.is_available() and dist.is_initialized()
     g = torch.Generator(device=dev).manual_seed(4242)
     kg = torch.Generator().manual_seed(4243)
+    # batch size: shard_n when given (tests: the exact per-rank share of an
+    # 8-GPU run), else --packets when changed from its c2 default, else the
+    # BASELINE size of the config
+    shard_n = getattr(args, "shard_n", None)
     if cfg == "c4":
-        n = args.packets if args.packets != 1 << 20 else 262_144
+        n = shard_n or (args.packets if args.packets != 1 << 20 else 262_144)
         L = 16384
         n_keys = 1
         lens = torch.full((n,), L, dtype=torch.int32)
     else:
-        n = args.packets if args.packets != 1 << 20 else 8 << 20
+        n = shard_n or (args.packets if args.packets != 1 << 20 else 8 << 20)
         n_keys = 65536
         lens = torch.randint(64, 4097, (n,), dtype=torch.int32, generator=kg)
     keys = torch.randint(0, 256, (n_keys, 64), dtype=torch.uint8, generator=kg).numpy()
@@ -541,6 +597,11 @@ def sharded_bench(cfg, args, world, rank, local, reps=3):
         return shard.sharded_call(work, buf, off, ln, rows=rows, row_specs=specs, balance=not uniform,
                                   device=dev, sync=torch.cuda.synchronize)
 
+    def run_piped(work, buf, off, ln, rows, specs, cap, out_specs):
+        return shard.sharded_call_pipelined(work, buf, off, ln, rows=rows, row_specs=specs, out_cap=cap,
+                                            out_row_specs=out_specs, chunks=args.sharded_chunks,
+                                            balance=not uniform, device=dev, sync=torch.cuda.synchronize)
+
     def max_times(t):
         v = torch.tensor([t["scatter_s"], t["compute_s"], t["gather_s"]], dtype=torch.float64, device=dev)
         if dist_on:
@@ -595,6 +656,26 @@ def sharded_bench(cfg, args, world, rank, local, reps=3):
             if r:
                 sums = [a + b for a, b in zip(sums, m)]
         sc, co, ga = (x / reps for x in sums)
+        # the same pass with the legs overlapped (shard.sharded_call_pipelined):
+        # its output must equal the serial pass's
+        piped_s = piped_ok = None
+        if dist_on and world > 1 and args.sharded_chunks > 0:
+            cap = tok_lengths if name == "encrypt" else (lambda x: (x - 48).clamp(min=0))
+            out_specs = [] if name == "encrypt" else [(torch.int32, 0), (torch.int32, 0)]
+            best = float("inf")
+            for r in range(reps + 1):
+                pout, pt_ = run_piped(work, buf, off, ln, rows, specs, cap, out_specs)
+                m = max_times({"scatter_s": 0.0, "compute_s": pt_["total_s"], "gather_s": 0.0})[1]
+                if r:
+                    best = min(best, m)
+            piped_s = best
+            if rank == 0:
+                gb_, go_, gl_, gr_ = out
+                pb_, po_, pl_, pr_ = pout
+                used = int(gl_.to(torch.int64).sum())
+                piped_ok = torch.equal(pb_[:used], gb_[:used]) and torch.equal(pl_, gl_.to(torch.int32)) and \
+                    all(torch.equal(a, b) for a, b in zip(pr_, gr_))
+                ok = ok and piped_ok
         total["scatter_s"] += sc
         total["compute_s"] += co
         total["gather_s"] += ga
@@ -630,7 +711,13 @@ def sharded_bench(cfg, args, world, rank, local, reps=3):
                                   "device_resident_packets_s": (h if name == "encrypt" else n - h) / co,
                                   "device_resident_gib_s": byts / co / 2**30,
                                   "end_to_end_packets_s": (h if name == "encrypt" else n - h) / (sc + co + ga),
+                                  "pipelined_ms": piped_s * 1e3 if piped_s else None,
+                                  "pipelined_chunks": args.sharded_chunks if piped_s else None,
+                                  "pipelined_end_to_end_packets_s":
+                                      (h if name == "encrypt" else n - h) / piped_s if piped_s else None,
+                                  "pipelined_equals_serial": piped_ok,
                                   "xgmi_scatter_gb_s": None, "xgmi_gather_gb_s": None}
+        total["pipelined_s"] = total.get("pipelined_s", 0.0) + (piped_s or 0.0)
     pkts = n
     byts_all = int(lens.to(torch.int64).sum())
     report.update({
@@ -639,6 +726,11 @@ def sharded_bench(cfg, args, world, rank, local, reps=3):
         "end_to_end_packets_s": pkts / (total["scatter_s"] + total["compute_s"] + total["gather_s"]),
         "scatter_ms": total["scatter_s"] * 1e3, "compute_ms": total["compute_s"] * 1e3,
         "gather_ms": total["gather_s"] * 1e3, "key_broadcast_setup_ms": keys_ms, "scaling": "strong", "ok": ok,
+        "pipelined_ms": total.get("pipelined_s", 0.0) * 1e3 or None,
+        "pipelined_end_to_end_packets_s": pkts / total["pipelined_s"] if total.get("pipelined_s") else None,
+        "pipelined_note": (f"shard.sharded_call_pipelined, {args.sharded_chunks} chunks per rank: the inputs of chunk "
+                           f"k and the outputs of chunk k-2 move in one grouped RCCL batch while chunk k-1 computes; "
+                           f"best of {reps} passes, max over ranks; output checked equal to the serial pass's"),
         "data": "synthetic random plaintext, IVs and keys generated on rank 0's device",
     })
     report["config"] = {
@@ -660,17 +752,21 @@ def sharded_bench(cfg, args, world, rank, local, reps=3):
 BASELINE_METRIC = "device-resident packets/s + GiB/s AES-256-CBC+HMAC-SHA256 at 1/2/4/8 MI355X"
 
 
-# Issue-cost model of the c2 kernels: SIMD-cycles per wave of
-# 64 packets of 500 B, single key, from the loop bodies' instruction mix
-# (tools/asm_mix.py on the round-2 ISA) priced with tools/cost_probe.hip's
-# measured costs (profiles/r02a_cost_probe.txt).
-ISSUE_CYCLES_PER_WAVE_PACKET_500B = {
-    # quad 0 (AES only) + 7 loop quads (AES + SHA) + 3 finishing compressions
-    "encrypt": (5083 + 1523) + 7 * (9888 + 1523) + 3 * 4827,
-    # 8 quads (AES + SHA of the same quad) + 2 finishing compressions
-    "decrypt": 8 * (10057 + 1523) + 2 * 4798,
+# Issue-slot model of the c2 kernels.  gfx950 gives
+# each SIMD one VALU issue per 4 cycles; two full-rate VGPR-only ops of two
+# waves may share it (dual issue, counted by SQ_ACTIVE_INST_VALU2), while every
+# 4-cycle form (v_perm, v_alignbit, v_add3), a pair of SGPR-reading ops and
+# each LDS instruction takes a slot alone (tools/issue_model_probe.hip,
+# profiles/r03a/r03b_issue_model_probe.txt).  Slots per wave of 64 packets of
+# 500 B from the ISA (tools/asm_mix.py --slots on the round-3 kernels):
+#   encrypt: quad 0 (AES only) + 7 loop quads (AES + SHA) + 3 compressions
+#   decrypt: 8 loop quads + 2 compressions
+# "floor": every dual-issuable op paired; "ceiling": none paired.
+SLOTS_PER_WAVE_PACKET_500B = {
+    "encrypt": {"floor": 1929 + 7 * 3030 + 3 * 1102, "ceiling": 2290 + 7 * 3666 + 3 * 1385},
+    "decrypt": {"floor": 8 * 3039 + 2 * 1095, "ceiling": 8 * 3724 + 2 * 1375},
 }
-# The same per-wave-packet composition measured instead of priced: the
+# The same per-wave-packet composition measured instead of counted: the
 # kernels' own enc_quad / dec_quad / sha256_compress in register-only loops
 # at c2's launch shape (tools/floor_probe.hip, profiles/r02af_floor_probe.txt;
 # SIMD-cycles per wave-iteration: enc quad 12 583, quad 0 8 381, dec quad at
@@ -681,21 +777,37 @@ CORE_CYCLES_PER_WAVE_PACKET_500B = {
 }
 
 
-def issue_model(kernel, n, L, keys, n_cu, ms, clock_ghz):
-    """Floor of the dominant kernel from its issue cost (c2 shape only)."""
+def issue_model(kernel, n, L, keys, n_cu, ms, clock_ghz, pmc=None):
+    """Issue-slot bounds of the dominant kernel (c2 shape only), and with the
+    committed PMC summary of the same kernel (``pmc``: its counters) the slots
+    it actually issued: SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2 + SQ_INSTS_LDS."""
     if L != 500 or keys != 1 or not clock_ghz:
         return None
-    waves_per_simd = n / 64 / (n_cu * 4)
-    cycles = ISSUE_CYCLES_PER_WAVE_PACKET_500B[kernel] * waves_per_simd
-    floor_ms = cycles / (clock_ghz * 1e9) * 1e3
+    n_simd = n_cu * 4
+    waves_per_simd = n / 64 / n_simd
+    sl = SLOTS_PER_WAVE_PACKET_500B[kernel]
+    floor = 4 * sl["floor"] * waves_per_simd
+    ceiling = 4 * sl["ceiling"] * waves_per_simd
     core = CORE_CYCLES_PER_WAVE_PACKET_500B[kernel] * waves_per_simd
-    core_ms = core / (clock_ghz * 1e9) * 1e3
-    return {"floor_cycles_per_simd": cycles, "clock_ghz": clock_ghz, "floor_ms": floor_ms,
-            "frac_of_issue_floor": floor_ms / ms,
-            "floor_ms_at_2p4ghz": cycles / 2.4e9 * 1e3,
-            "measured_core": {"cycles_per_simd": core, "ms": core_ms, "frac": core_ms / ms,
-                              "source": "tools/floor_probe.hip (the kernel's own quad/compression code from "
-                                        "registers only, no memory or packet loop), profiles/r02af_floor_probe.txt"}}
+    ms_at = lambda cyc: cyc / (clock_ghz * 1e9) * 1e3   # noqa: E731
+    out = {"model": "issue slots: one per SIMD per 4 cycles; two dual-issuable VALU ops of two waves may share one",
+           "clock_ghz": clock_ghz,
+           "floor_cycles_per_simd": floor, "floor_ms": ms_at(floor), "frac_of_floor": ms_at(floor) / ms,
+           "floor_ms_at_2p4ghz": floor / 2.4e9 * 1e3,
+           "ceiling_cycles_per_simd": ceiling, "ceiling_ms": ms_at(ceiling),
+           "measured_core": {"cycles_per_simd": core, "ms": ms_at(core), "frac": ms_at(core) / ms,
+                             "source": "tools/floor_probe.hip (the kernel's own quad/compression code from "
+                                       "registers only, no memory or packet loop), profiles/r02af_floor_probe.txt"}}
+    if pmc:
+        try:
+            slots = (pmc["SQ_INSTS_VALU"] - pmc["SQ_ACTIVE_INST_VALU2"] + pmc["SQ_INSTS_LDS"]) / n_simd
+            cyc = pmc["GRBM_GUI_ACTIVE"] / 8
+            out["pmc"] = {"issued_slots_per_simd": slots, "slot_cycles": 4 * slots, "kernel_cycles_per_xcd": cyc,
+                          "slot_cycles_over_kernel_cycles": 4 * slots / cyc,
+                          "dual_issued_frac_of_valu": 2 * pmc["SQ_ACTIVE_INST_VALU2"] / pmc["SQ_INSTS_VALU"]}
+        except (KeyError, TypeError, ZeroDivisionError):
+            pass
+    return out
 
 
 def _newest_pmc(kernel, n, L, keys):
@@ -755,14 +867,22 @@ def traffic_from_profiles(kernel, n, L, keys):
     return None
 
 
-def e2e_rate(ks, pt_dev, iv_dev, L, tl, n, stream, reps=3, chunks=32, n_streams=3):
+def e2e_rate(ks, pt_dev, iv_dev, L, tl, n, stream, reps=3, chunks=32, n_streams=3, sync_all=None,
+             reduce_max=None, world=1):
     """Host memory in, host memory out, pinned buffers:
     * serial: H2D of plaintext + IVs, encrypt, D2H of the tokens, one stream
       (and the mirror for decrypt: H2D of the tokens, decrypt, D2H);
     * pipelined: the batch cut into `chunks` slices issued round-robin on
       `n_streams` streams, so one slice's H2D, another's kernel and a third's
       D2H overlap (PCIe is full duplex).
-    Best of `reps`; the round trip is checked on the host copies."""
+    Best of `reps`; the round trip is checked on the host copies.
+
+    N > 1 (VERDICT r02 missing #1): every rank runs this at once on its own
+    shard from its own pinned host buffers over its own PCIe link, as the
+    packets of a Reticulum node arrive from its interfaces' socket buffers
+    (TCPInterface.py:392-401 -> Link.py:1161-1182).  ``sync_all`` (a barrier)
+    starts every rep on all ranks together and ``reduce_max`` takes each
+    rep's slowest rank, so ``aggregate`` = world x n packets / that time."""
     import torch
     from reticulum_amd import device
     dev = pt_dev.device
@@ -799,25 +919,42 @@ def e2e_rate(ks, pt_dev, iv_dev, L, tl, n, stream, reps=3, chunks=32, n_streams=
                 back_h[a:b].copy_(back_d[a:b], non_blocking=True)
 
     def timed(fn, parts):
-        best = float("inf")
+        own, slowest = [], []
         for _ in range(reps):
             torch.cuda.synchronize()
+            if sync_all is not None:
+                sync_all()
             t0 = time.perf_counter()
             fn(parts)
             torch.cuda.synchronize()
-            best = min(best, time.perf_counter() - t0)
-        return best
+            own.append(time.perf_counter() - t0)
+        slowest = reduce_max(own) if reduce_max is not None else own
+        return min(own), min(slowest)
 
-    res = {}
+    res, agg = {}, {}
     for name, parts in (("serial", 1), ("pipelined", chunks)):
         back_h.zero_()
-        te, td = timed(enc, parts), timed(dec, parts)
+        (te, te_all), (td, td_all) = timed(enc, parts), timed(dec, parts)
         ok = bool((st == 0).all()) and torch.equal(back_h[:, :L], pt_h)
         res[name] = {"encrypt_packets_s": n / te, "decrypt_packets_s": n / td, "roundtrip_packets_s": n / (te + td),
                      "encrypt_gib_s": n * L / te / 2**30, "decrypt_gib_s": n * L / td / 2**30,
                      "encrypt_pcie_gb_s": n * (L + 16 + tl) / te / 1e9, "ok": ok}
+        agg[name] = {"encrypt_packets_s": world * n / te_all, "decrypt_packets_s": world * n / td_all,
+                     "roundtrip_packets_s": world * n / (te_all + td_all),
+                     "encrypt_gib_s": world * n * L / te_all / 2**30, "decrypt_gib_s": world * n * L / td_all / 2**30,
+                     "ok_all": ok}
     res["note"] = (f"pinned host buffers; serial = H2D + kernel + D2H on one stream; pipelined = {chunks} slices "
                    f"round-robin on {n_streams} streams; best of {reps}")
+    if world > 1:
+        flags = reduce_max([0.0 if (res["serial"]["ok"] and res["pipelined"]["ok"]) else 1.0])
+        for name in agg:
+            agg[name]["ok_all"] = flags[0] == 0.0
+        agg["ranks"] = world
+        agg["note"] = (f"host-origin rate of the node: all {world} ranks at once, each on its own {n}-packet shard "
+                       f"from its own pinned host buffers over its own PCIe link; each rep starts on a barrier and "
+                       f"counts at its slowest rank; best of {reps} reps of world x n packets / that time. The "
+                       f"per-rank fields above are rank 0's own view")
+        res["aggregate"] = agg
     return res
 
 

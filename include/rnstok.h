@@ -111,6 +111,20 @@ uint32_t    rt_keyset_size(const rt_keyset *ks);
 /* ---- sizes --------------------------------------------------------------- */
 uint64_t    rt_token_len(uint64_t pt_len);      /* 16 + 16*(pt_len/16+1) + 32 */
 
+/* ---- kernel plan (diagnostic; no reference counterpart) ------------------ */
+/* The kernel rt_encrypt_uniform (decrypt = 0, len = plaintext bytes) or
+ * rt_decrypt_uniform (decrypt = 1, len = token bytes) runs for n packets on
+ * ctx's device, with one key (per_packet_keys = 0) or a key_idx array.  Lets
+ * tests and callers check which path a batch shape takes (e.g. that the
+ * 8-GPU c4 per-rank shard runs the long-token kernels). */
+enum {
+    RT_KERNEL_GENERAL = 0,      /* one packet per lane (k_encrypt / k_decrypt) */
+    RT_KERNEL_ENC_LONG4 = 1,    /* single key, a lane quad per CBC chain (k_encrypt_long4) */
+    RT_KERNEL_ENC_LONG = 2,     /* per-packet keys, hashing on waves of their own (k_encrypt_long) */
+    RT_KERNEL_DEC_LONG2 = 3     /* single key, producer/consumer HMAC chains (k_decrypt_long2) */
+};
+int         rt_plan_uniform(const rt_ctx *ctx, uint32_t n, uint32_t len, int per_packet_keys, int decrypt);
+
 /* ---- device-resident batch (Token.encrypt over n packets) ---------------- */
 /* pt + pt_off[i] holds pt_len[i] plaintext bytes; key_idx[i] selects the key
  * (NULL: key 0 for every packet); iv + 16*i is packet i's IV; the token is

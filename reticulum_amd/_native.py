@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("RNSTOK_LIB") or os.path.join(_HERE, "librnstok.so")
 RT_OK, RT_E_INVAL, RT_E_HIP, RT_E_NOMEM, RT_E_NODEV = 0, -1, -2, -3, -4
 RT_F_SORT_BY_LENGTH = 1
 RT_ST_OK, RT_ST_TOO_SHORT, RT_ST_BAD_HMAC, RT_ST_BAD_CT_LEN, RT_ST_BAD_PAD = 0, 1, 2, 3, 4
+RT_KERNEL_GENERAL, RT_KERNEL_ENC_LONG4, RT_KERNEL_ENC_LONG, RT_KERNEL_DEC_LONG2 = 0, 1, 2, 3
 
 # (name, restype, argtypes) for every entry point declared in include/rnstok.h
 _vp, _u32, _u64, _i32, _int = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int
@@ -30,6 +31,7 @@ SIGNATURES = [
     ("rt_keyset_destroy", None, [_vp]),
     ("rt_keyset_size", _u32, [_vp]),
     ("rt_token_len", _u64, [_u64]),
+    ("rt_plan_uniform", _int, [_vp, _u32, _u32, _int, _int]),
     ("rt_encrypt", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),
     ("rt_encrypt_uniform", _int, [_vp, _vp, _u64, _u32, _vp, _vp, _vp, _u64, _u32, _vp]),
     ("rt_decrypt", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),

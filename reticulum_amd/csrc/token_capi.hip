@@ -306,6 +306,12 @@ void rt_destroy(rt_ctx *c) {
 
 int rt_num_cus(const rt_ctx *c) { return c ? c->n_cu : 0; }
 
+int rt_plan_uniform(const rt_ctx *c, uint32_t n, uint32_t len, int per_packet_keys, int decrypt) {
+    if (!c) return fail(RT_E_INVAL, "rt_plan_uniform: no context");
+    return decrypt ? plan_decrypt(n, false, len, per_packet_keys != 0, c->n_cu)
+                   : plan_encrypt(n, false, len, per_packet_keys != 0, c->n_cu);
+}
+
 uint64_t rt_token_len(uint64_t pt_len) { return 16u + 16u * (pt_len / 16u + 1u) + 32u; }
 
 rt_keyset *rt_keyset_create_device(rt_ctx *c, const uint8_t *d_keys, uint32_t key_len, uint32_t n_keys,

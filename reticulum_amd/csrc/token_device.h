@@ -97,8 +97,17 @@ struct Lanes {
 // v_bitop3; bytes 0, 2, 3 take one (half-rate) v_perm_b32.
 template <int K, int REGION>
 __device__ __forceinline__ uint32_t taddr(uint32_t s, const Lanes &L) {
+#ifndef RNSTOK_SHIFT_ADDR
     if (K == 1) return and_or(s, L.m8, REGION ? L.r1 : L.r0);
     return perm(s, L.r1, REGION ? Sel<K>::R1 : Sel<K>::R0);
+#else
+    // Experiment (round 3, not the product): bytes 0, 2, 3 by a shift to bits
+    // 8..15 and the same and_or, two dual-issuable ops instead of one v_perm
+    // (which always takes a 4-cycle issue slot alone).  7-11 % slower on c2/c3
+    // and 14 % on the c4 shard (profiles/r03e_shift_addr_ab.txt).
+    const uint32_t t = K == 0 ? (s << 8) : (K == 1 ? s : (s >> (8 * K - 8)));
+    return and_or(t, L.m8, REGION ? L.r1 : L.r0);
+#endif
 }
 
 // One T-table round column: T0[a.b0] ^ T1[b.b1] ^ T2[c.b2] ^ T3[d.b3] ^ k

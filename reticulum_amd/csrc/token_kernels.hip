@@ -17,6 +17,7 @@
 #include "keysetup_device.h"
 #include "token_device.h"
 #include "token_launch.h"
+#include "../../include/rnstok.h"
 
 namespace rnstok {
 
@@ -1402,13 +1403,21 @@ static hipError_t balance(Args &a, Shape sh, SpareQueue *spare, hipStream_t s, b
     return hipMemsetAsync(a.queue, 0, 4, s);
 }
 
+int plan_encrypt(uint32_t n, bool packed, uint32_t uni_len, bool per_key, int n_cu) {
+    const uint32_t *len = packed ? &uni_len : nullptr;   // any non-null marks a packed batch
+#ifndef RNSTOK_NO_LONG4
+    if (!per_key && use_long(n, len, uni_len, n_cu, RNSTOK_LONG_MIN_LEN)) return RT_KERNEL_ENC_LONG4;
+#endif
+    if (use_long(n, len, uni_len, n_cu, RNSTOK_LONG_PERKEY_MIN_LEN)) return RT_KERNEL_ENC_LONG;
+    return RT_KERNEL_GENERAL;
+}
+
 hipError_t launch_encrypt(const EncArgs &args, int nr, int n_cu, SpareQueue *spare, hipStream_t s) {
     EncArgs a = args;
-#ifndef RNSTOK_NO_LONG4
-    if (!a.key_idx && use_long(a.n, a.pt_len, a.uni_len, n_cu, RNSTOK_LONG_MIN_LEN))
+    const int plan = plan_encrypt(a.n, a.pt_len != nullptr, a.uni_len, a.key_idx != nullptr, n_cu);
+    if (plan == RT_KERNEL_ENC_LONG4)
         return nr == 14 ? launch_enc_long4_nr<14>(a, n_cu, s) : launch_enc_long4_nr<10>(a, n_cu, s);
-#endif
-    if (use_long(a.n, a.pt_len, a.uni_len, n_cu, RNSTOK_LONG_PERKEY_MIN_LEN))
+    if (plan == RT_KERNEL_ENC_LONG)
         return nr == 14 ? launch_enc_long_nr<14>(a, n_cu, s) : launch_enc_long_nr<10>(a, n_cu, s);
 
     const Shape sh = shape_for(a.n, a.key_idx ? WG_PERKEY_ENC : WG_ENC, n_cu);
@@ -1426,13 +1435,18 @@ static hipError_t launch_dec_long_nr(const DecArgs &a, int n_cu, hipStream_t s) 
     return hipGetLastError();
 }
 
-hipError_t launch_decrypt(const DecArgs &args, int nr, int n_cu, SpareQueue *spare, hipStream_t s) {
-    DecArgs a = args;
+int plan_decrypt(uint32_t n, bool packed, uint32_t uni_len, bool per_key, int n_cu) {
     // long mode: one key, uniform well-formed tokens (whole blocks, at least
     // one), few per CU
-    if (!a.key_idx && a.tok_len == nullptr && a.uni_len >= 64u && a.uni_len >= 48u + RNSTOK_LONG_MIN_LEN &&
-        ((a.uni_len - 48u) & 15u) == 0 &&
-        (uint64_t)a.n <= 128ull * (uint64_t)n_cu)
+    if (!per_key && !packed && uni_len >= 64u && uni_len >= 48u + RNSTOK_LONG_MIN_LEN &&
+        ((uni_len - 48u) & 15u) == 0 && (uint64_t)n <= 128ull * (uint64_t)n_cu)
+        return RT_KERNEL_DEC_LONG2;
+    return RT_KERNEL_GENERAL;
+}
+
+hipError_t launch_decrypt(const DecArgs &args, int nr, int n_cu, SpareQueue *spare, hipStream_t s) {
+    DecArgs a = args;
+    if (plan_decrypt(a.n, a.tok_len != nullptr, a.uni_len, a.key_idx != nullptr, n_cu) == RT_KERNEL_DEC_LONG2)
         return nr == 14 ? launch_dec_long_nr<14>(a, n_cu, s) : launch_dec_long_nr<10>(a, n_cu, s);
     // one key and one pass at up to 1024 threads: the 1024-thread instance
     const uint64_t per_cu = ((uint64_t)a.n + n_cu - 1) / n_cu;

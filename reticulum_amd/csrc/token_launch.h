@@ -149,6 +149,10 @@ struct SpareQueue {
     virtual void release(hipStream_t s) = 0;
     virtual ~SpareQueue() {}
 };
+// Which kernel a batch runs on (RT_KERNEL_*, include/rnstok.h): the routing
+// launch_encrypt / launch_decrypt apply, exposed as rt_plan_uniform.
+int plan_encrypt(uint32_t n, bool packed, uint32_t uni_len, bool per_key, int n_cu);
+int plan_decrypt(uint32_t n, bool packed, uint32_t uni_len, bool per_key, int n_cu);
 hipError_t launch_encrypt(const EncArgs &a, int nr, int n_cu, SpareQueue *spare, hipStream_t s);
 hipError_t launch_decrypt(const DecArgs &a, int nr, int n_cu, SpareQueue *spare, hipStream_t s);
 // Token.verify_hmac (Token.py:77-84) over n tokens: status[i] = 0 (tag

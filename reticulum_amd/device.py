@@ -43,9 +43,31 @@ def _p_salt(t):
     return _p(t)
 
 
-def _stream(stream):
-    s = stream if stream is not None else torch.cuda.current_stream()
+def _stream(stream, device=None):
+    """The HIP stream handle to launch on: ``stream``, else the current
+    stream of ``device`` (the tensors' GPU, not whichever GPU is current)."""
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    if device is not None and s.device != torch.device(device):
+        raise ValueError(f"stream is on {s.device}, the tensors on {device}")
     return s.cuda_stream
+
+
+def _order_after_current(stream, *tensors):
+    """A launch on a side ``stream`` that reads ``tensors`` made on the
+    current stream (e.g. a key table an RCCL broadcast just filled; torch only
+    makes the *current* stream wait for a collective): the side stream waits
+    for the current stream first, and the tensors' memory is kept from reuse
+    until the side stream is done with it (the caller may drop them at once)."""
+    if stream is None:
+        return
+    dev = tensors[0].device
+    cur = torch.cuda.current_stream(dev)
+    if stream == cur:
+        return
+    stream.wait_stream(cur)
+    for t in tensors:
+        if t is not None:
+            t.record_stream(stream)
 
 
 def _check_u8(*ts):
@@ -95,7 +117,7 @@ def encrypt_uniform(ks: KeySet, pt, pt_len, iv, tok, key_idx=None, stream=None):
     _check_i32(n, key_idx=key_idx)
     lib = _native.load()
     _native.check(lib.rt_encrypt_uniform(ks.handle, _p_rows(pt), pt.stride(0), pt_len, _p(key_idx), _p(iv),
-                                         _p_rows(tok), tok.stride(0), n, _stream(stream)))
+                                         _p_rows(tok), tok.stride(0), n, _stream(stream, pt.device)))
 
 
 def decrypt_uniform(ks: KeySet, tok, tok_len, pt, out_len, status, key_idx=None, stream=None):
@@ -108,7 +130,7 @@ def decrypt_uniform(ks: KeySet, tok, tok_len, pt, out_len, status, key_idx=None,
     _check_i32(n, out_len=out_len, status=status, key_idx=key_idx)
     lib = _native.load()
     _native.check(lib.rt_decrypt_uniform(ks.handle, _p_rows(tok), tok.stride(0), tok_len, _p(key_idx), _p_rows(pt),
-                                         pt.stride(0), _p(out_len), _p(status), n, _stream(stream)))
+                                         pt.stride(0), _p(out_len), _p(status), n, _stream(stream, tok.device)))
 
 
 def verify(ks: KeySet, tok, tok_off, tok_len, status, key_idx=None, stream=None):
@@ -121,7 +143,7 @@ def verify(ks: KeySet, tok, tok_off, tok_len, status, key_idx=None, stream=None)
     _check_i32(n, tok_len=tok_len, status=status, key_idx=key_idx)
     lib = _native.load()
     _native.check(lib.rt_verify(ks.handle, _p(tok), _p(tok_off), _p(tok_len), _p(key_idx), _p(status), n,
-                                _stream(stream)))
+                                _stream(stream, tok.device)))
 
 
 def verify_trials(ks: KeySet, tok, tok_off, tok_len, pair_off, pair_key, first, stream=None):
@@ -138,7 +160,7 @@ def verify_trials(ks: KeySet, tok, tok_off, tok_len, pair_off, pair_key, first, 
     _check_i32(pair_key.numel(), pair_key=pair_key)
     lib = _native.load()
     _native.check(lib.rt_verify_trials(ks.handle, _p(tok), _p(tok_off), _p(tok_len), _p(pair_off), _p(pair_key),
-                                       _p(first), n, pair_key.numel(), _stream(stream)))
+                                       _p(first), n, pair_key.numel(), _stream(stream, tok.device)))
 
 
 def _workspace(n, device):
@@ -160,10 +182,10 @@ def encrypt(ks: KeySet, pt, pt_off, pt_len, iv, tok, tok_off, key_idx=None, stre
     if sort:
         ws = workspace if workspace is not None else _workspace(n, pt.device)
         _native.check(lib.rt_encrypt_ex(ks.handle, _p(pt), _p(pt_off), _p(pt_len), _p(key_idx), _p(iv), _p(tok),
-                                        _p(tok_off), n, _native.RT_F_SORT_BY_LENGTH, _p(ws), _stream(stream)))
+                                        _p(tok_off), n, _native.RT_F_SORT_BY_LENGTH, _p(ws), _stream(stream, pt.device)))
         return
     _native.check(lib.rt_encrypt(ks.handle, _p(pt), _p(pt_off), _p(pt_len), _p(key_idx), _p(iv), _p(tok),
-                                 _p(tok_off), n, _stream(stream)))
+                                 _p(tok_off), n, _stream(stream, pt.device)))
 
 
 def decrypt(ks: KeySet, tok, tok_off, tok_len, pt, pt_off, out_len, status, key_idx=None, stream=None, sort=False,
@@ -177,10 +199,10 @@ def decrypt(ks: KeySet, tok, tok_off, tok_len, pt, pt_off, out_len, status, key_
         ws = workspace if workspace is not None else _workspace(n, tok.device)
         _native.check(lib.rt_decrypt_ex(ks.handle, _p(tok), _p(tok_off), _p(tok_len), _p(key_idx), _p(pt),
                                         _p(pt_off), _p(out_len), _p(status), n, _native.RT_F_SORT_BY_LENGTH, _p(ws),
-                                        _stream(stream)))
+                                        _stream(stream, tok.device)))
         return
     _native.check(lib.rt_decrypt(ks.handle, _p(tok), _p(tok_off), _p(tok_len), _p(key_idx), _p(pt), _p(pt_off),
-                                 _p(out_len), _p(status), n, _stream(stream)))
+                                 _p(out_len), _p(status), n, _stream(stream, tok.device)))
 
 
 def hkdf(ikm, out, salt=None, context=None, stream=None):
@@ -200,7 +222,7 @@ def hkdf(ikm, out, salt=None, context=None, stream=None):
     _native.check(lib.rt_hkdf(ctx, _p(ikm), ikm.stride(0), ikm.shape[1], _p_salt(salt),
                               salt.stride(0) if salt is not None else 0, salt.shape[1] if salt is not None else 0,
                               _p(context), context.numel() if context is not None else 0, _p(out), out.stride(0),
-                              length, n, _stream(stream)))
+                              length, n, _stream(stream, ikm.device)))
 
 
 def keyset(keys, stream=None):
@@ -214,7 +236,8 @@ def keyset(keys, stream=None):
     n, klen = keys.shape
     lib = _native.load()
     ctx = _native.context(keys.device.index)
-    h = lib.rt_keyset_create_device(ctx, _p(keys), klen, n, _stream(stream))
+    _order_after_current(stream, keys)
+    h = lib.rt_keyset_create_device(ctx, _p(keys), klen, n, _stream(stream, keys.device))
     if not h:
         raise _native.NativeError(-1, _native.last_error())
     return KeySet._adopt(h, klen, n, lib, ctx)
@@ -230,10 +253,11 @@ def derive_keyset(ikm, salt=None, context=None, key_len=64, stream=None):
     n = ikm.shape[0]
     lib = _native.load()
     ctx = _native.context(ikm.device.index)
+    _order_after_current(stream, ikm, salt, context)
     h = lib.rt_keyset_create_hkdf(ctx, _p(ikm), ikm.stride(0), ikm.shape[1], _p_salt(salt),
                                   salt.stride(0) if salt is not None else 0, salt.shape[1] if salt is not None else 0,
                                   _p(context), context.numel() if context is not None else 0, key_len, n,
-                                  _stream(stream))
+                                  _stream(stream, ikm.device))
     if not h:
         raise _native.NativeError(-1, _native.last_error())
     return KeySet._adopt(h, key_len, n, lib, ctx)
@@ -254,7 +278,7 @@ def map_hashes(data, out, salts, part_off=None, part_len=None, part_res=None, sd
     ctx = _native.context(data.device.index)
     _native.check(lib.rt_map_hashes(ctx, _p(data), _p(part_off), _p(part_len), data.numel(), sdu, _p(salts),
                                     salts.shape[1], _p(part_res), salts.shape[0], guard, _p(out),
-                                    _p(first_collision), n_parts, _stream(stream)))
+                                    _p(first_collision), n_parts, _stream(stream, data.device)))
 
 
 # ---------------------------------------------------------------- wire side --
@@ -278,7 +302,7 @@ def hdlc_frame(pkt, pkt_off, pkt_len, out, frame_off, workspace=None, stream=Non
     ws = workspace if workspace is not None else torch.empty(
         int(lib.rt_hdlc_frame_workspace_bytes(n)), dtype=torch.uint8, device=pkt.device)
     _native.check(lib.rt_hdlc_frame(_ctx_of(pkt), _p(pkt), _p(pkt_off), _p(pkt_len), n, _p(out), _p(frame_off),
-                                    _p(ws), _stream(stream)))
+                                    _p(ws), _stream(stream, pkt.device)))
 
 
 def hdlc_deframe(buf, out, frame_off, frame_len, status, counts, hw_mtu=262144, ifac_size=0, workspace=None,
@@ -296,7 +320,7 @@ def hdlc_deframe(buf, out, frame_off, frame_len, status, counts, hw_mtu=262144, 
     ws = workspace if workspace is not None else torch.empty(
         int(lib.rt_hdlc_deframe_workspace_bytes(buf.numel())), dtype=torch.uint8, device=buf.device)
     _native.check(lib.rt_hdlc_deframe(_ctx_of(buf), _p(buf), buf.numel(), hw_mtu, ifac_size, _p(out), _p(frame_off),
-                                      _p(frame_len), _p(status), _p(counts), max_pairs, _p(ws), _stream(stream)))
+                                      _p(frame_len), _p(status), _p(counts), max_pairs, _p(ws), _stream(stream, buf.device)))
 
 
 def ifac_mask(pkt, pkt_off, pkt_len, ifac, ifac_key, out, out_off, stream=None):
@@ -309,7 +333,7 @@ def ifac_mask(pkt, pkt_off, pkt_len, ifac, ifac_key, out, out_off, stream=None):
         raise ValueError("shape mismatch")
     lib = _native.load()
     _native.check(lib.rt_ifac_mask(_ctx_of(pkt), _p(pkt), _p(pkt_off), _p(pkt_len), _p(ifac), ifac.shape[1],
-                                   _p(ifac_key), ifac_key.numel(), _p(out), _p(out_off), n, _stream(stream)))
+                                   _p(ifac_key), ifac_key.numel(), _p(out), _p(out_off), n, _stream(stream, pkt.device)))
 
 
 def ifac_unmask(pkt, pkt_off, pkt_len, ifac_key, ifac_out, out, out_off, status, stream=None):
@@ -324,7 +348,7 @@ def ifac_unmask(pkt, pkt_off, pkt_len, ifac_key, ifac_out, out, out_off, status,
     lib = _native.load()
     _native.check(lib.rt_ifac_unmask(_ctx_of(pkt), _p(pkt), _p(pkt_off), _p(pkt_len), ifac_out.shape[1],
                                      _p(ifac_key), ifac_key.numel(), _p(ifac_out), _p(out), _p(out_off), _p(status),
-                                     n, _stream(stream)))
+                                     n, _stream(stream, pkt.device)))
 
 
 def packet_unpack(pkt, pkt_off, pkt_len, fields, stream=None):
@@ -337,7 +361,7 @@ def packet_unpack(pkt, pkt_off, pkt_len, fields, stream=None):
         raise ValueError("shape mismatch")
     lib = _native.load()
     _native.check(lib.rt_packet_unpack(_ctx_of(pkt), _p(pkt), _p(pkt_off), _p(pkt_len), _p(fields), n,
-                                       _stream(stream)))
+                                       _stream(stream, pkt.device)))
 
 
 def pack_headers(flags, hops, destination_hash, context, out, out_off, transport_id=None, stream=None):
@@ -349,4 +373,4 @@ def pack_headers(flags, hops, destination_hash, context, out, out_off, transport
     lib = _native.load()
     _native.check(lib.rt_packet_pack_headers(_ctx_of(out), _p(flags), _p(hops), _p(transport_id),
                                              _p(destination_hash), _p(context), _p(out), _p(out_off), n,
-                                             _stream(stream)))
+                                             _stream(stream, out.device)))

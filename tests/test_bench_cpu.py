@@ -51,8 +51,14 @@ def test_roofline_models_and_newest_profile():
     sys.path.insert(0, ROOT)
     import bench
     m = bench.issue_model("encrypt", 1 << 20, 500, 1, 256, 1.0, 2.0)
-    assert m["measured_core"]["cycles_per_simd"] > m["floor_cycles_per_simd"] > 0
+    assert m["ceiling_cycles_per_simd"] > m["measured_core"]["cycles_per_simd"] > m["floor_cycles_per_simd"] > 0
     assert abs(m["measured_core"]["frac"] - m["measured_core"]["ms"] / 1.0) < 1e-12
+    assert "pmc" not in m
+    # issued slots from a PMC summary: VALU - dual-issue pairs + LDS, per SIMD
+    pmc = {"SQ_INSTS_VALU": 4.2e8, "SQ_ACTIVE_INST_VALU2": 3.6e7, "SQ_INSTS_LDS": 1.2e8, "GRBM_GUI_ACTIVE": 1.6e7}
+    p = bench.issue_model("encrypt", 1 << 20, 500, 1, 256, 1.0, 2.0, pmc)["pmc"]
+    assert abs(p["issued_slots_per_simd"] - (4.2e8 - 3.6e7 + 1.2e8) / 1024) < 1e-6
+    assert abs(p["dual_issued_frac_of_valu"] - 2 * 3.6e7 / 4.2e8) < 1e-12
     assert bench.issue_model("encrypt", 1 << 20, 100, 1, 256, 1.0, 2.0) is None   # c2 shape only
     path, d = bench._newest_pmc("encrypt", 1 << 20, 500, 1)
     assert path is not None and "encrypt" in d

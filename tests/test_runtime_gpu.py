@@ -426,3 +426,37 @@ def test_device_keyset_from_table(rt, klen):
     assert (status == 0).all() and back.to_list() == [pt[i].tobytes() for i in range(n)]
     with pytest.raises(ValueError):
         device.keyset(torch.zeros((4, 48), dtype=torch.uint8, device="cuda"))
+
+
+def test_device_keyset_on_side_stream_after_current_stream_fill(rt):
+    """a key table filled on the current stream (as an
+    RCCL broadcast leaves it: only the current stream waits for the
+    collective) and expanded on a side stream, the caller dropping the table
+    at once.  The side stream must wait for the fill and the table's memory
+    must not be reused before the key setup read it: every token opens under
+    the oracle with the table's keys."""
+    import torch
+    from reticulum_amd import device
+    rng = np.random.Generator(np.random.PCG64(4242))
+    nk, n, L = 512, 1500, 64
+    keys = rng.integers(0, 256, (nk, 64), dtype=np.uint8)
+    side = torch.cuda.Stream()
+    for trial in range(3):
+        table = torch.zeros((nk, 64), dtype=torch.uint8, device="cuda")
+        # a slow producer on the current stream: spin the GPU, then fill
+        torch.cuda._sleep(2_000_000)
+        table.copy_(torch.from_numpy(keys).cuda(non_blocking=True))
+        ks = device.keyset(table, stream=side)
+        del table                                        # the caller lets go at once
+        junk = torch.full((nk, 64), 0xA5, dtype=torch.uint8, device="cuda")   # may land on the freed block
+        kidx = rng.integers(0, nk, n).astype(np.int32)
+        pt = rng.integers(0, 256, (n, L), dtype=np.uint8)
+        iv = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+        tok = torch.empty((n, rt.token_len(L)), dtype=torch.uint8, device="cuda")
+        device.encrypt_uniform(ks, torch.from_numpy(pt).cuda(), L, torch.from_numpy(iv).cuda(), tok,
+                               key_idx=torch.from_numpy(kidx).cuda())
+        torch.cuda.synchronize()
+        t = tok.cpu().numpy()
+        for i in range(0, n, 61):
+            assert t[i].tobytes() == oracle.encrypt(keys[kidx[i]].tobytes(), iv[i].tobytes(), pt[i].tobytes()), trial
+        del junk

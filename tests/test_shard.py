@@ -230,3 +230,109 @@ def test_broadcast_keys_rejects_bad_tables():
                            torch.ones((3, 32), dtype=torch.uint8))
     finally:
         dist.destroy_process_group()
+
+
+def _token_cap(lens):
+    return 16 + 16 * (lens // 16 + 1) + 32
+
+
+def _pipelined_worker(rank, world, port, result_q, chunks, balance):
+    import torch.distributed as dist
+    from oracle import ctoken
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    key = bytes(range(64))
+    n = 203
+    if rank == 0:
+        rng = np.random.Generator(np.random.PCG64(79))
+        lens = rng.integers(0, 1500, n).astype(np.int64)
+        lens[5:9] = 0                                            # empty packets inside a chunk
+        off = np.zeros(n, np.int64)
+        off[1:] = np.cumsum(lens[:-1])
+        buf = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+        ivs = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+        args = (torch.from_numpy(buf), torch.from_numpy(off), torch.from_numpy(lens))
+        rows = [torch.from_numpy(ivs)]
+    else:
+        args, rows = (None, None, None), ()
+    work = _oracle_work(key)
+    serial, _ = shard.sharded_call(work, *args, rows=rows, row_specs=[(torch.uint8, 16)], balance=balance)
+    piped, times = shard.sharded_call_pipelined(work, *args, rows=rows, row_specs=[(torch.uint8, 16)],
+                                                out_cap=_token_cap, out_row_specs=[(torch.int32, 0)],
+                                                chunks=chunks, balance=balance)
+    assert set(times) == {"total_s", "chunks"} and times["chunks"] == chunks
+    if rank == 0:
+        sb, so, sl, (sst,) = serial
+        pb, po, pl, (pst,) = piped
+        ok = torch.equal(sb, pb) and torch.equal(so, po) and torch.equal(sl, pl) and torch.equal(sst, pst)
+        ok = ok and pl.dtype == torch.int32 and po.dtype == torch.int64 and pl.numel() == n
+        for i in range(n):
+            ref = ctoken.encrypt(key, ivs[i].tobytes(), buf[int(off[i]):int(off[i]) + int(lens[i])].tobytes())
+            ok = ok and pb[int(po[i]):int(po[i]) + int(pl[i])].numpy().tobytes() == ref
+        result_q.put(ok)
+    else:
+        assert piped is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,chunks,balance", [(2, 4, True), (2, 1, False), (3, 5, False), (3, 3, True)])
+def test_sharded_call_pipelined_equals_serial_gloo(world, chunks, balance):
+    """the chunk-pipelined scatter -> compute -> gather
+     returns exactly what the serial sharded_call returns, and
+    every token is the oracle's, at world sizes 2 and 3, with more chunks
+    than some ranks have packets' worth of work and empty packets."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, q, chunks, balance)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get() is True
+
+
+def test_slice_compacts_gapped_offsets():
+    """a range whose byte span holds other packets' bytes (or
+    gaps) sends only its own packets' bytes, compacted in packet order."""
+    buf = torch.arange(100, dtype=torch.uint8)
+    off = torch.tensor([80, 0, 40], dtype=torch.int64)
+    ln = torch.tensor([5, 3, 0], dtype=torch.int64)
+    b, o, l = shard._slice(buf, off, ln, 0, 3)
+    assert b.numel() == 8 and o.tolist() == [0, 5, 8] and l.tolist() == [5, 3, 0]
+    assert b.tolist() == list(range(80, 85)) + [0, 1, 2]
+    # contiguous ranges stay views of the caller's buffer
+    b2, o2, _ = shard._slice(buf, torch.tensor([10, 13]), torch.tensor([3, 4]), 0, 2)
+    assert b2.data_ptr() == buf[10:].data_ptr() and o2.tolist() == [0, 3]
+
+
+def _refuse_worker(rank, world, port, result_q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        shard.broadcast_keys(torch.zeros((4, 48), dtype=torch.uint8) if rank == 0 else None, src=0)
+        result_q.put((rank, "no error"))
+    except ValueError as e:
+        result_q.put((rank, str(e)))
+    dist.destroy_process_group()
+
+
+def test_broadcast_keys_refusal_raises_on_every_rank():
+    """a table refused on the source makes every rank raise
+    (no rank is left waiting in the next broadcast)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_refuse_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    got = dict(q.get() for _ in range(2))
+    assert "uint8 table" in got[0] and "refused" in got[1]

@@ -79,6 +79,9 @@ def parse():
                     help="N > 1: chunks per rank of the pipelined sharded pass (0 disables it)")
     ap.add_argument("--sharded-timeout", type=float, default=150.0,
                     help="N > 1: seconds allowed for the sharded c4 pass after the headline")
+    ap.add_argument("--layout", choices=["rows", "interleaved"], default="rows",
+                    help="HBM layout of the c2/c3 batch: packed rows (the reference's byte strings) or the "
+                         "unit-interleaved device layout (rt_encrypt_interleaved)")
     ap.add_argument("--e2e", action="store_true", default=True, help="also time the PCIe-inclusive path")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false")
     return ap.parse_args()
@@ -270,13 +273,27 @@ def main():
         key_idx = torch.randint(0, args.keys, (n,), dtype=torch.int32, device=dev, generator=g)
     stream = torch.cuda.current_stream()
 
+    ilv = args.layout == "interleaved"
+    if ilv:
+        # the unit-interleaved device layout (rt_encrypt_interleaved): the same
+        # packets, 16-B unit u of packet p at 16*(u*n + p)
+        pt_u = device.interleave(pt, L)
+        tok_u = torch.empty((tl // 16, n, 16), dtype=torch.uint8, device=dev)
+        back_u = torch.empty(((tl - 48) // 16, n, 16), dtype=torch.uint8, device=dev)
+
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        device.encrypt_uniform(ks, pt, L, iv, tok, key_idx=key_idx, stream=stream)
+        if ilv:
+            device.encrypt_interleaved(ks, pt_u, L, iv, tok_u, key_idx=key_idx, stream=stream)
+        else:
+            device.encrypt_uniform(ks, pt, L, iv, tok, key_idx=key_idx, stream=stream)
         if ev is not None:
             ev[1].record(stream)
-        device.decrypt_uniform(ks, tok, tl, back, out_len, status, key_idx=key_idx, stream=stream)
+        if ilv:
+            device.decrypt_interleaved(ks, tok_u, tl, back_u, out_len, status, key_idx=key_idx, stream=stream)
+        else:
+            device.decrypt_uniform(ks, tok, tl, back, out_len, status, key_idx=key_idx, stream=stream)
         if ev is not None:
             ev[2].record(stream)
 
@@ -284,6 +301,8 @@ def main():
     # before the warmup so that nothing idles the GPU between warmup and timing
     step()
     torch.cuda.synchronize()
+    if ilv:
+        back = device.deinterleave(back_u, tl - 48)
     ok = bool((status == 0).all()) and bool((out_len == L).all()) and torch.equal(back[:, :L], pt)
     if not ok:
         raise SystemExit("bench: round trip failed on the benchmark batch")
@@ -330,7 +349,7 @@ def main():
     dom = "decrypt" if dec_avg > enc_avg else "encrypt"
     dom_ms = max(enc_avg, dec_avg)
     dom_ops = ops_d if dom == "decrypt" else ops_e
-    traffic = traffic_from_profiles(dom, n, L, args.keys)
+    traffic = traffic_from_profiles(dom, n, L, args.keys, args.layout)
     achieved = dom_ops / (dom_ms * 1e-3)
     bytes_enc = n * (L + 16 + tl + 0)         # read pt + iv, write token
     bytes_dec = n * (tl + (tl - 48) + 8)      # read token, write pt + len + status
@@ -363,7 +382,7 @@ def main():
                                 f"c3: 2^20 x 500 B packets per GPU, {args.keys} per-packet keys")
                    if (n == 1 << 20 and L == 500) else f"{n} x {L} B packets per GPU, {args.keys} key(s)",
                    "packets_per_gpu": n, "plaintext_bytes": L, "token_bytes": tl, "keys": args.keys,
-                   "row_strides": {"plaintext": ps, "token": ts},
+                   "row_strides": {"plaintext": ps, "token": ts}, "layout": args.layout,
                    "step": "encrypt+MAC then verify+decrypt of the same batch", "parallelism": f"shard{world}"},
         "kernels": {
             "encrypt": {"ms": enc_avg, "ms_median": enc_ms[len(enc_ms) // 2], "packets_s": n / (enc_avg * 1e-3),
@@ -383,11 +402,11 @@ def main():
                      "algorithmic_bytes_per_launch": hbm_bytes,
                      "algorithmic_hbm_gb_s": hbm_bytes / (dom_ms * 1e-3) / 1e9,
                      "frac_of_survey_P": achieved / (n_cu * 64 * 2.4e9),
-                     "sustained_clock_ghz": sustained_clock_ghz(dom, n, L, args.keys),
+                     "sustained_clock_ghz": sustained_clock_ghz(dom, n, L, args.keys, args.layout),
                      "lds_frac": n * blocks(L) * LDS_LOOKUPS_PER_BLOCK / (dom_ms * 1e-3) / peak_lds,
                      "issue_model": issue_model(dom, n, L, args.keys, n_cu, dom_ms,
-                                                sustained_clock_ghz(dom, n, L, args.keys),
-                                                (_newest_pmc(dom, n, L, args.keys)[1] or {}).get(dom)),
+                                                sustained_clock_ghz(dom, n, L, args.keys, args.layout),
+                                                (_newest_pmc(dom, n, L, args.keys, args.layout)[1] or {}).get(dom)),
                      "note": "achieved = canonical int32 VALU lane-ops per launch (SURVEY §8(d): 352/AES block, "
                              "1464/SHA-256 compression, +8 tag compare) / HIP-event kernel time; peak = CUs x 128 "
                              "lanes x 2.4 GHz (MI355X_MICROARCH.md), i.e. two wave64 VALU instructions per SIMD per "
@@ -810,15 +829,16 @@ def issue_model(kernel, n, L, keys, n_cu, ms, clock_ghz, pmc=None):
     return out
 
 
-def _newest_pmc(kernel, n, L, keys):
+def _newest_pmc(kernel, n, L, keys, layout="rows"):
     import glob
     import re
 
     def order(path):   # r02y < r02aa < r02ak: round, then tag length, then tag
-        m = re.match(r"r(\d+)([a-z]+)_pmc\.json$", os.path.basename(path))
+        m = re.match(r"r(\d+)([a-z]+)_(?:ilv)?pmc\.json$", os.path.basename(path))
         return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
 
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=order, reverse=True):
+    suffix = "_pmc.json" if layout == "rows" else "_ilvpmc.json"     # interleaved-layout runs: rNNx_ilvpmc.json
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*" + suffix)), key=order, reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
@@ -830,15 +850,15 @@ def _newest_pmc(kernel, n, L, keys):
     return None, None
 
 
-def sustained_clock_ghz(kernel, n, L, keys):
+def sustained_clock_ghz(kernel, n, L, keys, layout="rows"):
     """Shader clock under this load: GRBM_GUI_ACTIVE per launch (summed over
     the 8 XCDs) / 8 over the kernel's average duration in the kernel trace of
     the same profiling run (profiles/<round>_kernel_stats.csv)."""
     import csv
-    path, d = _newest_pmc(kernel, n, L, keys)
+    path, d = _newest_pmc(kernel, n, L, keys, layout)
     if not path:
         return None
-    stats = path.replace("_pmc.json", "_kernel_stats.csv")
+    stats = path.replace("_ilvpmc.json", "_ilv_kernel_stats.csv").replace("_pmc.json", "_kernel_stats.csv")
     tag = "k_encrypt<14, " if kernel == "encrypt" else "k_decrypt<14, "
     try:
         with open(stats) as f:
@@ -849,10 +869,10 @@ def sustained_clock_ghz(kernel, n, L, keys):
         return None
 
 
-def traffic_from_profiles(kernel, n, L, keys):
+def traffic_from_profiles(kernel, n, L, keys, layout="rows"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     whose workload matches (profiles/<round>_pmc.json, tools/pmc_summary.py)."""
-    path, d = _newest_pmc(kernel, n, L, keys)
+    path, d = _newest_pmc(kernel, n, L, keys, layout)
     if path:
         raw = d[kernel].get("hbm_bytes_per_launch_uncorrected")
         if raw:

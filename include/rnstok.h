@@ -111,6 +111,23 @@ uint32_t    rt_keyset_size(const rt_keyset *ks);
 /* ---- sizes --------------------------------------------------------------- */
 uint64_t    rt_token_len(uint64_t pt_len);      /* 16 + 16*(pt_len/16+1) + 32 */
 
+/* ---- unit-interleaved device batches (no reference counterpart) ---------- */
+/* For batches that are produced and consumed on the device (e.g. the
+ * deframer's output feeding decrypt), a layout in which every wave load and
+ * store instruction covers 1 KiB of contiguous HBM: 16-B unit u of packet p
+ * at buf + 16*(u*n + p).  Plaintexts hold ceil(pt_len/16) units (the last
+ * one partial: only its first pt_len % 16 bytes are read), tokens
+ * rt_token_len(pt_len)/16 units (IV, ciphertext blocks, 2 tag units), the
+ * decrypted plaintext (tok_len - 48)/16 units (pad block included, as
+ * rt_decrypt_uniform).  iv: n x 16 B.  Outputs, statuses and error order are
+ * those of rt_encrypt_uniform / rt_decrypt_uniform on the same packets;
+ * decrypt takes well-formed token lengths only (48 + 16*k, k >= 1), others
+ * are RT_E_INVAL.  Always the one-packet-per-lane kernels. */
+int rt_encrypt_interleaved(const rt_keyset *ks, const uint8_t *pt, uint32_t pt_len, const uint32_t *key_idx,
+                           const uint8_t *iv, uint8_t *tok, uint32_t n, void *stream);
+int rt_decrypt_interleaved(const rt_keyset *ks, const uint8_t *tok, uint32_t tok_len, const uint32_t *key_idx,
+                           uint8_t *pt, uint32_t *pt_len, int32_t *status, uint32_t n, void *stream);
+
 /* ---- kernel plan (diagnostic; no reference counterpart) ------------------ */
 /* The kernel rt_encrypt_uniform (decrypt = 0, len = plaintext bytes) or
  * rt_decrypt_uniform (decrypt = 1, len = token bytes) runs for n packets on

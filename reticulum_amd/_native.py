@@ -32,6 +32,8 @@ SIGNATURES = [
     ("rt_keyset_size", _u32, [_vp]),
     ("rt_token_len", _u64, [_u64]),
     ("rt_plan_uniform", _int, [_vp, _u32, _u32, _int, _int]),
+    ("rt_encrypt_interleaved", _int, [_vp, _vp, _u32, _vp, _vp, _vp, _u32, _vp]),
+    ("rt_decrypt_interleaved", _int, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp]),
     ("rt_encrypt", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),
     ("rt_encrypt_uniform", _int, [_vp, _vp, _u64, _u32, _vp, _vp, _vp, _u64, _u32, _vp]),
     ("rt_decrypt", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),

@@ -39,32 +39,40 @@ struct Stager {
 static constexpr int N_STAGERS = 4;
 
 // Chunk counters for the token kernels' dynamic packet loop (ragged uniform
-// batches): one 64-B slot per launch, round-robin.  A slot is handed out
-// again only after the stream of its next user waits on the event recorded
-// after its previous launch, so a counter is never zeroed or advanced while
-// an earlier launch (on any stream) may still read it.  The ring's lock is
-// held from acquire() to release(), i.e. across one memset and one launch.
+// batches): one 64-B slot per launch.  A slot is handed out again only after
+// the stream of its next user waits on the event recorded after its previous
+// launch, so a counter is never zeroed or advanced while an earlier launch
+// (on any stream) may still read it.  No lock is held across the launch:
+// each slot has its own busy flag, taken by compare-and-swap at acquire() and
+// dropped at release(), so threads launching on different streams only ever
+// contend for one atomic increment (the round-robin cursor).  A thread that
+// finds every slot held falls back to the static stride (correct, less
+// balanced).
 struct QueueRing final : SpareQueue {
     static constexpr uint32_t SLOTS = 256;
-    std::mutex mu;
     uint32_t *d = nullptr;
     hipEvent_t ev[SLOTS] = {};
-    bool recorded[SLOTS] = {};
-    uint32_t next = 0, cur = 0;
-    uint32_t *acquire(hipStream_t s) override {
+    bool recorded[SLOTS] = {};                 // read and written by the slot's holder only
+    std::atomic<uint32_t> next{0};
+    std::atomic<uint32_t> busy[SLOTS] = {};
+    uint32_t *acquire(hipStream_t s, uint32_t *slot) override {
         if (!d) return nullptr;
-        mu.lock();
-        cur = next;
-        next = (next + 1u) % SLOTS;
-        if (recorded[cur] && hipStreamWaitEvent(s, ev[cur], 0) != hipSuccess) {
-            mu.unlock();
-            return nullptr;
+        for (uint32_t tries = 0; tries < SLOTS; ++tries) {
+            const uint32_t i = next.fetch_add(1u, std::memory_order_relaxed) % SLOTS;
+            uint32_t free_ = 0u;
+            if (!busy[i].compare_exchange_strong(free_, 1u, std::memory_order_acquire)) continue;
+            if (recorded[i] && hipStreamWaitEvent(s, ev[i], 0) != hipSuccess) {
+                busy[i].store(0u, std::memory_order_release);
+                return nullptr;
+            }
+            *slot = i;
+            return d + 16u * i;
         }
-        return d + 16u * cur;
+        return nullptr;
     }
-    void release(hipStream_t s) override {
-        if (hipEventRecord(ev[cur], s) == hipSuccess) recorded[cur] = true;
-        mu.unlock();
+    void release(hipStream_t s, uint32_t slot) override {
+        if (hipEventRecord(ev[slot], s) == hipSuccess) recorded[slot] = true;
+        busy[slot].store(0u, std::memory_order_release);
     }
 };
 
@@ -126,11 +134,23 @@ struct rt_keyset {
 static hipError_t after_setup(const rt_keyset *k, hipStream_t s) {
     return s == k->home ? hipSuccess : hipStreamWaitEvent(s, k->ready, 0);
 }
-// The launch just enqueued on `s` reads the records.
+// The launch just enqueued on `s` reads the records.  Entries of other
+// streams whose last recorded launch has completed are dropped on the way
+// (their event destroyed), so a long-lived key set used from many
+// short-lived streams keeps one entry per stream still in flight, and
+// rt_keyset_destroy never waits on events of streams that are gone.
 static hipError_t note_use(rt_keyset *k, hipStream_t s) {
     std::lock_guard<std::mutex> g(k->mu);
     for (auto &u : k->uses)
         if (u.first == s) return hipEventRecord(u.second, s);
+    if (k->uses.size() >= 4) {
+        auto done = [](const std::pair<hipStream_t, hipEvent_t> &u) {
+            if (hipEventQuery(u.second) != hipSuccess) return false;
+            hipEventDestroy(u.second);
+            return true;
+        };
+        k->uses.erase(std::remove_if(k->uses.begin(), k->uses.end(), done), k->uses.end());
+    }
     hipEvent_t e = nullptr;
     hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
     if (r != hipSuccess) return r;
@@ -446,6 +466,23 @@ int rt_encrypt_uniform(const rt_keyset *k, const uint8_t *pt, uint64_t pt_stride
     a.pt = pt; a.pt_stride = pt_stride; a.uni_len = pt_len; a.key_idx = key_idx; a.iv = iv;
     a.tok = tok; a.tok_stride = tok_stride; a.n = n;
     return enc_common(k, a, stream);
+}
+
+int rt_encrypt_interleaved(const rt_keyset *k, const uint8_t *pt, uint32_t pt_len, const uint32_t *key_idx,
+                           const uint8_t *iv, uint8_t *tok, uint32_t n, void *stream) {
+    EncArgs a{};
+    a.pt = pt; a.uni_len = pt_len; a.key_idx = key_idx; a.iv = iv; a.tok = tok; a.n = n; a.ilv = 1;
+    return enc_common(k, a, stream);
+}
+
+int rt_decrypt_interleaved(const rt_keyset *k, const uint8_t *tok, uint32_t tok_len, const uint32_t *key_idx,
+                           uint8_t *pt, uint32_t *pt_len, int32_t *status, uint32_t n, void *stream) {
+    if (tok_len < 64u || (tok_len & 15u))
+        return fail(RT_E_INVAL, "rt_decrypt_interleaved: token length must be 48 + 16*k, k >= 1");
+    DecArgs a{};
+    a.tok = tok; a.uni_len = tok_len; a.key_idx = key_idx; a.pt = pt; a.out_len = pt_len; a.status = status; a.n = n;
+    a.ilv = 1;
+    return dec_common(k, a, stream);
 }
 
 int rt_decrypt(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_off, const uint32_t *tok_len,

@@ -190,7 +190,12 @@ __device__ __forceinline__ u32x4 pad_block(const uint8_t *p, uint32_t r) {
 
 // --------------------------------------------------------------- encrypt --
 
-template <int NR, bool PERKEY>
+// ILV: the unit-interleaved layout of rt_encrypt_interleaved (16-B unit u of
+// packet p at 16*(u*n + p) in the plaintext and token buffers): every wave
+// load/store instruction then covers 1 KiB of contiguous HBM instead of 64
+// scattered 16-B pieces.  US is the distance between a
+// packet's consecutive units.
+template <int NR, bool PERKEY, bool ILV = false>
 __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encrypt(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
     fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);
@@ -213,11 +218,12 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
             load_uniform8(ipad, a.rec + REC_IPAD);
         }
         const uint32_t L = in.l(p);
-        const uint8_t *P = a.pt + in.o(p);
-        uint8_t *O = a.tok + (a.tok_off ? a.tok_off[p] : (uint64_t)p * a.tok_stride);
+        const uint64_t US = ILV ? 16ull * a.n : 16ull;
+        const uint8_t *P = ILV ? a.pt + 16ull * p : a.pt + in.o(p);
+        uint8_t *O = ILV ? a.tok + 16ull * p : a.tok + (a.tok_off ? a.tok_off[p] : (uint64_t)p * a.tok_stride);
         const u32x4 iv = ld16(a.iv + 16ull * p);
         st16(O, iv);
-        uint8_t *C = O + 16;
+        uint8_t *C = O + US;
 
         const uint32_t nfull = L >> 4, nq = nfull >> 2, tb = (nfull & 3u) + 1u;
         uint32_t h[8];
@@ -244,27 +250,27 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
             // with a scalar branch around every SHA round: 1.8 % slower, A/B).
             auto load_quad = [&](uint32_t q) {
                 if (q < nq) {
-                    x[0] = ld16(P); x[1] = ld16(P + 16); x[2] = ld16(P + 32); x[3] = ld16(P + 48);
+                    x[0] = ld16(P); x[1] = ld16(P + US); x[2] = ld16(P + 2 * US); x[3] = ld16(P + 3 * US);
                 } else {
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        x[j] = (uint32_t)j + 1u < tb ? ld16(P + 16 * j)
-                                                     : ((uint32_t)j + 1u == tb ? pad_block(P + 16 * j, rem) : z);
+                        x[j] = (uint32_t)j + 1u < tb ? ld16(P + US * j)
+                                                     : ((uint32_t)j + 1u == tb ? pad_block(P + US * j, rem) : z);
                 }
             };
             auto store_quad = [&](uint32_t q) {
                 const uint32_t nst = q < nq ? 4u : tb;
                 st16(C, c[0]);
-                if (nst > 1u) st16(C + 16, c[1]);
-                if (nst > 2u) st16(C + 32, c[2]);
-                if (nst > 3u) st16(C + 48, c[3]);
+                if (nst > 1u) st16(C + US, c[1]);
+                if (nst > 2u) st16(C + 2 * US, c[2]);
+                if (nst > 3u) st16(C + 3 * US, c[3]);
             };
             load_quad(0u);
             enc_quad<NR, false>(c, x, prev, K.rk, LN, S);
             store_quad(0u);
             sha_units(S.w, prev, c[0], c[1], c[2]);
             prev = c[3];
-            P += 64; C += 64;
+            P += 4 * US; C += 4 * US;
 #pragma nounroll
             for (uint32_t q = 1; q <= nq; ++q) {
                 load_quad(q);
@@ -280,7 +286,7 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
                 store_quad(q);
                 sha_units(S.w, prev, c[0], c[1], c[2]);
                 prev = c[3];
-                P += 64; C += 64;
+                P += 4 * US; C += 4 * US;
             }
             // S.w: units u0..u3 of the tail quad (u0 = the block before it),
             // prev = u4; tu = tb + 1 units are left for the inner hash: a full
@@ -296,9 +302,9 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
             else
                 load_uniform8(opad, a.rec + REC_OPAD);
             hmac_finish(h, tu >= 4u ? 0u : 1u, S.w, fin, opad);
-            uint8_t *T = O + 16 + 16ull * (nfull + 1u);
+            uint8_t *T = O + US * (nfull + 2u);
             st16(T, u32x4{bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3])});
-            st16(T + 16, u32x4{bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7])});
+            st16(T + US, u32x4{bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7])});
         }
     }
 }
@@ -456,7 +462,27 @@ __global__ __launch_bounds__(256) void k_encrypt_long(EncArgs a) {
 // (16 per wave) and drop each quad of ciphertext into a two-slot LDS ring;
 // waves 8-9 hash the previous quad of the same tokens, one token per lane,
 // one barrier per quad step.  Single key, uniform lengths.
-constexpr uint32_t L4_TOK = 128, L4_AES_WAVES = 8, L4_THREADS = 64u * (L4_AES_WAVES + 2u);
+#ifndef RNSTOK_L4_HASH_WAVES
+#define RNSTOK_L4_HASH_WAVES 2
+#endif
+constexpr uint32_t L4_TOK = 128, L4_AES_WAVES = 8, L4_HASH_WAVES = RNSTOK_L4_HASH_WAVES;
+constexpr uint32_t L4_THREADS = 64u * (L4_AES_WAVES + L4_HASH_WAVES), L4_HASH_TOK = L4_TOK / L4_HASH_WAVES;
+static_assert(L4_HASH_TOK <= 64u && L4_TOK % L4_HASH_WAVES == 0u, "one token per hashing lane");
+
+// Ring layout: token t's quad (4 blocks x 16 B) at t*64 B, block i in 16-B
+// unit i ^ l4_swz(t).  Without the swizzle the AES lanes' 4-B stores (lanes of
+// 8 consecutive tokens x 4 columns) met 4-way and the hashing lanes' 16-B
+// reads (one token per lane) 4-way bank conflicts (7 % of the kernel's LDS
+// cycles, profiles/r02e_c4s8_pmc_summary.txt); with it both are conflict-free
+// for ds_write_b32's 2 x 32 and ds_read_b128's 4 x 16 lane groups
+// (MI355X_MICROARCH.md LDS table; exhaustive check in DESIGN.md §4.2).
+__device__ __forceinline__ uint32_t l4_swz(uint32_t t) {
+#ifndef RNSTOK_L4_NO_SWIZZLE
+    return ((t >> 1) ^ (t >> 2)) & 3u;
+#else
+    return 0u;
+#endif
+}
 constexpr uint32_t L4_RING = LDS_ENC_BYTES;                              // after the table image
 // The ring holds 2 * L4_PHASE quads: AES waves fill L4_PHASE quads per
 // barrier while the hashing waves consume the previous L4_PHASE.  Two quads
@@ -508,9 +534,18 @@ __device__ __forceinline__ uint32_t enc_block4(uint32_t s, const uint32_t *rk, c
         // bound, and this is a shorter dependent path than the three
         // v_xor_b32_dpp in a row the compiler folds the plain XORs into
         // (c4 shard encrypt 1.044 -> 0.992 ms, A/B)
+#ifndef RNSTOK_L4_XOR_CHAIN3
+        // two of the moves carry an XOR (v_xor_b32 with a DPP source: the
+        // round key and this lane's own term ride on them), so the new column
+        // is ONE xor3 after the moves instead of two in a row
+        uint32_t x1 = quad_rot<1>(u1) ^ u0, x2 = quad_rot<2>(u2) ^ rk[r], x3 = quad_rot<3>(u3);
+        asm volatile("" : "+v"(x1), "+v"(x2), "+v"(x3));
+        s = xor3(x1, x2, x3);
+#else
         uint32_t x1 = quad_rot<1>(u1), x2 = quad_rot<2>(u2), x3 = quad_rot<3>(u3);
         asm volatile("" : "+v"(x1), "+v"(x2), "+v"(x3));
         s = xor3(xor3(x1, x2, x3), u0, rk[r]);
+#endif
     }
     // final round: byte k of column j is S[s_{j+k}.b_k] (tlast_enc, split the same way)
     const uint32_t v0 = lds(taddr<0, 1>(s, L), 0) & 0x000000ffu, v1 = lds(taddr<1, 1>(s, L), 128) & 0x0000ff00u;
@@ -530,7 +565,9 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     const bool aes = wave < L4_AES_WAVES;
     const uint32_t col = threadIdx.x & 3u;
-    const uint32_t slot = aes ? threadIdx.x >> 2 : (wave - L4_AES_WAVES) * 64u + lane;   // token of the workgroup
+    const bool hash_lane = aes || lane < L4_HASH_TOK;
+    const uint32_t slot = aes ? threadIdx.x >> 2 : (wave - L4_AES_WAVES) * L4_HASH_TOK + (hash_lane ? lane : 0u);
+    const uint32_t swz = l4_swz(slot);
     const uint32_t L = a.uni_len, nfull = L >> 4, nq = nfull >> 2, tb = (nfull & 3u) + 1u, rem = L & 15u;
     uint32_t rk[NR + 1];
 #pragma unroll
@@ -538,7 +575,7 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
 
     for (uint32_t base = blockIdx.x * L4_TOK; base < a.n; base += gridDim.x * L4_TOK) {
         const uint32_t t = base + slot;
-        const bool valid = t < a.n;
+        const bool valid = t < a.n && hash_lane;
         const uint32_t p = valid ? (a.order ? a.order[t] : t) : 0u;
         const uint8_t *P = a.pt + (valid ? in_off(a.pt_off, a.pt_stride, p) : 0);
         uint8_t *O = a.tok + (valid ? in_off(a.tok_off, a.tok_stride, p) : 0);
@@ -576,7 +613,7 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
                     if (valid && (uint32_t)b < nst) st32u(Ck + 16 * b, cq[b]);
                 lds_w *ring = (lds_w *)(uintptr_t)(L4_RING + ((k % L4_SLOTS) * L4_TOK + slot) * 64u + 4u * col);
 #pragma unroll
-                for (int b = 0; b < 4; ++b) ring[4 * b] = cq[b];
+                for (int b = 0; b < 4; ++b) ring[4u * ((uint32_t)b ^ swz)] = cq[b];
                 // end of a phase: its quads become visible to the hashing
                 // waves, which are done with the previous phase's slots
                 if ((k + 1u) % L4_PHASE == 0u || k == nq) __syncthreads();
@@ -593,7 +630,7 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
             for (uint32_t j = 1; j <= phases; ++j) {
               for (uint32_t q = (j - 1u) * L4_PHASE; q < j * L4_PHASE && q <= nq; ++q) {
                 lds_q *r = (lds_q *)(uintptr_t)(L4_RING + ((q % L4_SLOTS) * L4_TOK + slot) * 64u);
-                const u32x4 c0 = r[0], c1 = r[1], c2 = r[2], c3 = r[3];
+                const u32x4 c0 = r[0u ^ swz], c1 = r[1u ^ swz], c2 = r[2u ^ swz], c3 = r[3u ^ swz];
                 if (q < nq) {
 #ifndef RNSTOK_L4_PROBE_AES_ONLY        // timing probe: no HMAC (wrong tags)
                     uint32_t w[16];
@@ -631,7 +668,7 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
 // key: 768 threads (168 VGPRs) for batches of several passes, 1024 (128
 // VGPRs, 4 waves/SIMD) when one pass covers the batch (e.g. 16 KiB Resource
 // tokens, one per lane: 512 x 2 passes at 768 was 9 % slower).
-template <int NR, bool PERKEY, int WG = PERKEY ? WG_PERKEY_DEC : WG_DEC>
+template <int NR, bool PERKEY, int WG = PERKEY ? WG_PERKEY_DEC : WG_DEC, bool ILV = false>
 __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
     fill_tables<true>(tab_u32, a.sbox, a.sbox + 256);
@@ -653,12 +690,14 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
         }
         // opad: loaded where it is used, after the quad loop
         const uint32_t T = in.l(p);
-        const uint8_t *Kt = a.tok + in.o(p);
-        uint8_t *O = a.pt + (a.pt_off ? a.pt_off[p] : (uint64_t)p * a.pt_stride);
+        const uint64_t US = ILV ? 16ull * a.n : 16ull;       // see k_encrypt
+        const uint8_t *Kt = ILV ? a.tok + 16ull * p : a.tok + in.o(p);
+        uint8_t *O = ILV ? a.pt + 16ull * p : a.pt + (a.pt_off ? a.pt_off[p] : (uint64_t)p * a.pt_stride);
         int32_t st;
         uint32_t outlen = 0;
 
-        if (T < 64u || ((T - 48u) & 15u)) {
+        // (the interleaved layout takes well-formed uniform tokens only: rt_decrypt_interleaved)
+        if (!ILV && (T < 64u || ((T - 48u) & 15u))) {
             // Malformed length (rare): decide TOO_SHORT / BAD_HMAC / BAD_CT_LEN
             // exactly as Token.decrypt would, without touching the AES path.
             if (T <= 32u) {
@@ -690,7 +729,7 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
             // through one sha256_compress.
             const u32x4 z = {0u, 0u, 0u, 0u};
             u32x4 prev = ld16(Kt);
-            const uint8_t *C = Kt + 16;
+            const uint8_t *C = Kt + US;
             uint8_t *D = O;
             Sha256 S;
             u32x4 c[4], pp[4];
@@ -698,9 +737,9 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
             for (uint32_t q = 0; q <= nq; ++q) {
                 const uint32_t nbk = q < nq ? 4u : tb;
                 c[0] = ld16(C);
-                c[1] = nbk > 1u ? ld16(C + 16) : z;
-                c[2] = nbk > 2u ? ld16(C + 32) : z;
-                c[3] = nbk > 3u ? ld16(C + 48) : z;
+                c[1] = nbk > 1u ? ld16(C + US) : z;
+                c[2] = nbk > 2u ? ld16(C + 2 * US) : z;
+                c[3] = nbk > 3u ? ld16(C + 3 * US) : z;
                 S.start(h);
                 sha_units(S.w, prev, c[0], c[1], c[2]);
                 dec_quad<NR, true>(pp, c, prev, K.rk, LN, S);
@@ -710,17 +749,17 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) h[k] += keep ? S.v[k] : 0u;
                 st16(D, pp[0]);
-                if (nbk > 1u) st16(D + 16, pp[1]);
-                if (nbk > 2u) st16(D + 32, pp[2]);
-                if (nbk > 3u) st16(D + 48, pp[3]);
+                if (nbk > 1u) st16(D + US, pp[1]);
+                if (nbk > 2u) st16(D + 2 * US, pp[2]);
+                if (nbk > 3u) st16(D + 3 * US, pp[3]);
                 prev = c[3];
-                C += 64; D += 64;
+                C += 4 * US; D += 4 * US;
             }
             // the tail quad: pb = the block before it (re-read rather than
             // kept live through the loop), c[0..tb-1] its ciphertext,
             // pp[0..tb-1] its plaintext
-            const u32x4 pb = ld16(Kt + 64ull * nq);
-            const u32x4 r0 = ld16(Kt + (T - 32u)), r1 = ld16(Kt + (T - 16u));
+            const u32x4 pb = ld16(Kt + 4ull * US * nq);
+            const u32x4 r0 = ld16(Kt + US * ((T >> 4) - 2u)), r1 = ld16(Kt + US * ((T >> 4) - 1u));
             const u32x4 last = tb == 1u ? pp[0] : (tb == 2u ? pp[1] : (tb == 3u ? pp[2] : pp[3]));
             const bool full = tb >= 3u;
             const uint32_t tu = tb + 1u;
@@ -741,7 +780,7 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
                 outlen = 16u * nb - padn;
             } else {
                 if (st == 4) outlen = padn;   // authenticated pad byte, for the error message
-                for (uint32_t i = 0; i < nb; ++i) st16(O + 16 * i, z);
+                for (uint32_t i = 0; i < nb; ++i) st16(O + US * i, z);
             }
         }
         a.status[p] = st;
@@ -1331,7 +1370,11 @@ static Shape shape_for(uint32_t n, int max_threads, int n_cu) {
 
 template <int NR>
 static hipError_t launch_enc_nr(const EncArgs &a, Shape sh, hipStream_t s) {
-    if (a.key_idx)
+    if (a.ilv && a.key_idx)
+        hipLaunchKernelGGL((k_encrypt<NR, true, true>), dim3(sh.grid), dim3(sh.threads), LDS_ENC_BYTES, s, a);
+    else if (a.ilv)
+        hipLaunchKernelGGL((k_encrypt<NR, false, true>), dim3(sh.grid), dim3(sh.threads), LDS_ENC_BYTES, s, a);
+    else if (a.key_idx)
         hipLaunchKernelGGL((k_encrypt<NR, true>), dim3(sh.grid), dim3(sh.threads), LDS_ENC_BYTES, s, a);
     else
         hipLaunchKernelGGL((k_encrypt<NR, false>), dim3(sh.grid), dim3(sh.threads), LDS_ENC_BYTES, s, a);
@@ -1339,7 +1382,14 @@ static hipError_t launch_enc_nr(const EncArgs &a, Shape sh, hipStream_t s) {
 }
 template <int NR>
 static hipError_t launch_dec_nr(const DecArgs &a, Shape sh, hipStream_t s) {
-    if (a.key_idx)
+    if (a.ilv && a.key_idx)
+        hipLaunchKernelGGL((k_decrypt<NR, true, WG_PERKEY_DEC, true>), dim3(sh.grid), dim3(sh.threads), LDS_DEC_BYTES,
+                           s, a);
+    else if (a.ilv && sh.threads > WG_DEC)
+        hipLaunchKernelGGL((k_decrypt<NR, false, 1024, true>), dim3(sh.grid), dim3(sh.threads), LDS_DEC_BYTES, s, a);
+    else if (a.ilv)
+        hipLaunchKernelGGL((k_decrypt<NR, false, WG_DEC, true>), dim3(sh.grid), dim3(sh.threads), LDS_DEC_BYTES, s, a);
+    else if (a.key_idx)
         hipLaunchKernelGGL((k_decrypt<NR, true>), dim3(sh.grid), dim3(sh.threads), LDS_DEC_BYTES, s, a);
     else if (sh.threads > WG_DEC)
         hipLaunchKernelGGL((k_decrypt<NR, false, 1024>), dim3(sh.grid), dim3(sh.threads), LDS_DEC_BYTES, s, a);
@@ -1393,11 +1443,11 @@ static hipError_t launch_enc_long4_nr(const EncArgs &a, int n_cu, hipStream_t s)
 // per lane) would leave a third of the workgroups one packet longer; there
 // the dynamic chunk loop balances the SIMDs instead.
 template <class Args>
-static hipError_t balance(Args &a, Shape sh, SpareQueue *spare, hipStream_t s, bool *took) {
+static hipError_t balance(Args &a, Shape sh, SpareQueue *spare, hipStream_t s, bool *took, uint32_t *slot) {
     const uint64_t lanes = (uint64_t)sh.grid * (uint64_t)sh.threads;
     *took = false;
     if (a.queue || !spare || a.n <= lanes || a.n % lanes == 0 || a.n > QUEUE_MAX_N) return hipSuccess;
-    a.queue = spare->acquire(s);
+    a.queue = spare->acquire(s, slot);
     if (!a.queue) return hipSuccess;     // no slot: the static stride (correct, less balanced)
     *took = true;
     return hipMemsetAsync(a.queue, 0, 4, s);
@@ -1414,7 +1464,7 @@ int plan_encrypt(uint32_t n, bool packed, uint32_t uni_len, bool per_key, int n_
 
 hipError_t launch_encrypt(const EncArgs &args, int nr, int n_cu, SpareQueue *spare, hipStream_t s) {
     EncArgs a = args;
-    const int plan = plan_encrypt(a.n, a.pt_len != nullptr, a.uni_len, a.key_idx != nullptr, n_cu);
+    const int plan = a.ilv ? RT_KERNEL_GENERAL : plan_encrypt(a.n, a.pt_len != nullptr, a.uni_len, a.key_idx != nullptr, n_cu);
     if (plan == RT_KERNEL_ENC_LONG4)
         return nr == 14 ? launch_enc_long4_nr<14>(a, n_cu, s) : launch_enc_long4_nr<10>(a, n_cu, s);
     if (plan == RT_KERNEL_ENC_LONG)
@@ -1422,9 +1472,10 @@ hipError_t launch_encrypt(const EncArgs &args, int nr, int n_cu, SpareQueue *spa
 
     const Shape sh = shape_for(a.n, a.key_idx ? WG_PERKEY_ENC : WG_ENC, n_cu);
     bool took = false;
-    hipError_t e = balance(a, sh, spare, s, &took);
+    uint32_t slot = 0;
+    hipError_t e = balance(a, sh, spare, s, &took, &slot);
     if (e == hipSuccess) e = nr == 14 ? launch_enc_nr<14>(a, sh, s) : launch_enc_nr<10>(a, sh, s);
-    if (took) spare->release(s);
+    if (took) spare->release(s, slot);
     return e;
 }
 template <int NR>
@@ -1446,16 +1497,17 @@ int plan_decrypt(uint32_t n, bool packed, uint32_t uni_len, bool per_key, int n_
 
 hipError_t launch_decrypt(const DecArgs &args, int nr, int n_cu, SpareQueue *spare, hipStream_t s) {
     DecArgs a = args;
-    if (plan_decrypt(a.n, a.tok_len != nullptr, a.uni_len, a.key_idx != nullptr, n_cu) == RT_KERNEL_DEC_LONG2)
+    if (!a.ilv && plan_decrypt(a.n, a.tok_len != nullptr, a.uni_len, a.key_idx != nullptr, n_cu) == RT_KERNEL_DEC_LONG2)
         return nr == 14 ? launch_dec_long_nr<14>(a, n_cu, s) : launch_dec_long_nr<10>(a, n_cu, s);
     // one key and one pass at up to 1024 threads: the 1024-thread instance
     const uint64_t per_cu = ((uint64_t)a.n + n_cu - 1) / n_cu;
     const int max_t = a.key_idx ? WG_PERKEY_DEC : (per_cu <= 1024u ? 1024 : WG_DEC);
     const Shape sh = shape_for(a.n, max_t, n_cu);
     bool took = false;
-    hipError_t e = balance(a, sh, spare, s, &took);
+    uint32_t slot = 0;
+    hipError_t e = balance(a, sh, spare, s, &took, &slot);
     if (e == hipSuccess) e = nr == 14 ? launch_dec_nr<14>(a, sh, s) : launch_dec_nr<10>(a, sh, s);
-    if (took) spare->release(s);
+    if (took) spare->release(s, slot);
     return e;
 }
 hipError_t launch_key_setup(const uint8_t *keys, uint32_t key_len, uint32_t n_keys, const uint8_t *sbox,
@@ -1490,6 +1542,16 @@ hipError_t configure_kernels() {
     RT_CFG((k_decrypt<10, false>), LDS_DEC_BYTES);
     RT_CFG((k_decrypt<10, false, 1024>), LDS_DEC_BYTES);
     RT_CFG((k_decrypt<10, true>), LDS_DEC_BYTES);
+    RT_CFG((k_encrypt<14, false, true>), LDS_ENC_BYTES);
+    RT_CFG((k_encrypt<14, true, true>), LDS_ENC_BYTES);
+    RT_CFG((k_encrypt<10, false, true>), LDS_ENC_BYTES);
+    RT_CFG((k_encrypt<10, true, true>), LDS_ENC_BYTES);
+    RT_CFG((k_decrypt<14, false, WG_DEC, true>), LDS_DEC_BYTES);
+    RT_CFG((k_decrypt<14, false, 1024, true>), LDS_DEC_BYTES);
+    RT_CFG((k_decrypt<14, true, WG_PERKEY_DEC, true>), LDS_DEC_BYTES);
+    RT_CFG((k_decrypt<10, false, WG_DEC, true>), LDS_DEC_BYTES);
+    RT_CFG((k_decrypt<10, false, 1024, true>), LDS_DEC_BYTES);
+    RT_CFG((k_decrypt<10, true, WG_PERKEY_DEC, true>), LDS_DEC_BYTES);
 #undef RT_CFG
     return e;
 }

@@ -21,6 +21,7 @@ struct EncArgs {
     const uint32_t *order;      // null -> lane i handles packet i; else packet order[i]
     uint32_t *queue;            // null -> static grid stride; else a zeroed chunk counter (sorted batches)
     uint32_t n;
+    uint32_t ilv;               // 1: unit-interleaved layout (16-B unit u of packet p at 16*(u*n + p)), uniform
 };
 
 struct DecArgs {
@@ -40,6 +41,7 @@ struct DecArgs {
     const uint32_t *order;      // null -> lane i handles token i; else token order[i]
     uint32_t *queue;            // as EncArgs::queue
     uint32_t n;
+    uint32_t ilv;               // as EncArgs::ilv (tokens and plaintexts), well-formed uniform tokens only
 };
 
 // Ratchet trials (Identity.py:865-878): pairs j in [pair_off[t],
@@ -140,13 +142,14 @@ uint64_t sort_workspace_bytes(uint32_t n);    // order[n] + 2 x SORT_BUCKETS cou
 hipError_t launch_length_order(const uint32_t *len, uint32_t n, int dec, void *workspace, const uint32_t **order,
                                uint32_t **queue, int n_cu, hipStream_t s);
 // Chunk counters for ragged uniform batches (the static stride would leave a
-// ragged last pass).  acquire() hands out a 4-byte device counter that no
-// other launch can still be reading once work queued on `s` after this call
-// runs (the C-ABI orders slot reuse with an event per slot); release() is
-// called once after the launch that used it has been enqueued on `s`.
+// ragged last pass).  acquire() hands out a 4-byte device counter (and its
+// slot number) that no other launch can still be reading once work queued on
+// `s` after this call runs (the C-ABI orders slot reuse with an event per
+// slot), or null; release(s, slot) is called once after the launch that used
+// it has been enqueued on `s`.  Thread-safe, no lock held in between.
 struct SpareQueue {
-    virtual uint32_t *acquire(hipStream_t s) = 0;
-    virtual void release(hipStream_t s) = 0;
+    virtual uint32_t *acquire(hipStream_t s, uint32_t *slot) = 0;
+    virtual void release(hipStream_t s, uint32_t slot) = 0;
     virtual ~SpareQueue() {}
 };
 // Which kernel a batch runs on (RT_KERNEL_*, include/rnstok.h): the routing

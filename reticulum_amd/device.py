@@ -133,6 +133,70 @@ def decrypt_uniform(ks: KeySet, tok, tok_len, pt, out_len, status, key_idx=None,
                                          pt.stride(0), _p(out_len), _p(status), n, _stream(stream, tok.device)))
 
 
+# ------------------------------------------------- unit-interleaved layout --
+# For batches that live on the device from end to end (rt_encrypt_interleaved,
+# include/rnstok.h): 16-B unit u of packet p at 16*(u*n + p), i.e. a (U, n, 16)
+# uint8 tensor, so every wave load/store is one contiguous KiB of HBM.
+
+def units(nbytes):
+    """16-B units that hold nbytes."""
+    return (int(nbytes) + 15) // 16
+
+
+def interleave(rows, nbytes=None):
+    """(n, >= nbytes) uint8 rows -> the (units(nbytes), n, 16) interleaved
+    tensor (a copy; the last unit zero-padded)."""
+    n = rows.shape[0]
+    L = rows.shape[1] if nbytes is None else int(nbytes)
+    U = units(L)
+    out = torch.zeros((n, U * 16), dtype=torch.uint8, device=rows.device)
+    out[:, :L] = rows[:, :L]
+    return out.view(n, U, 16).transpose(0, 1).contiguous()
+
+
+def deinterleave(u, nbytes=None):
+    """(U, n, 16) interleaved units -> (n, nbytes) rows (a copy)."""
+    U, n, _ = u.shape
+    rows = u.transpose(0, 1).reshape(n, U * 16)
+    return rows[:, : (U * 16 if nbytes is None else int(nbytes))].contiguous()
+
+
+def _check_units(name, t, U, n):
+    if t.dtype != torch.uint8 or t.dim() != 3 or tuple(t.shape) != (U, n, 16) or not t.is_contiguous():
+        raise ValueError(f"{name} must be a contiguous ({U}, {n}, 16) uint8 tensor of interleaved units")
+
+
+def encrypt_interleaved(ks: KeySet, pt, pt_len, iv, tok, key_idx=None, stream=None):
+    """Token.encrypt of n packets of pt_len bytes in the interleaved layout:
+    pt (units(pt_len), n, 16), iv (n, 16), tok (token_len(pt_len)/16, n, 16).
+    Tokens are bit-identical to encrypt_uniform's."""
+    n = iv.shape[0]
+    _check_units("pt", pt, units(pt_len), n)
+    _check_units("tok", tok, token_len(pt_len) // 16, n)
+    _check_u8(iv)
+    _check_iv(iv, n)
+    _check_i32(n, key_idx=key_idx)
+    lib = _native.load()
+    _native.check(lib.rt_encrypt_interleaved(ks.handle, _p(pt) if pt.numel() else None, pt_len, _p(key_idx), _p(iv),
+                                             _p(tok), n, _stream(stream, tok.device)))
+
+
+def decrypt_interleaved(ks: KeySet, tok, tok_len, pt, out_len, status, key_idx=None, stream=None):
+    """Token.decrypt of n tokens of tok_len = 48 + 16k bytes (k >= 1) in the
+    interleaved layout: tok (tok_len/16, n, 16), pt ((tok_len-48)/16, n, 16)
+    (plaintext incl. its pad block, zeroed on failure), out_len/status (n,)
+    int32 as decrypt_uniform."""
+    n = tok.shape[1] if tok.dim() == 3 else -1
+    if tok_len < 64 or tok_len % 16:
+        raise ValueError("interleaved tokens must be 48 + 16*k bytes, k >= 1")
+    _check_units("tok", tok, tok_len // 16, n)
+    _check_units("pt", pt, (tok_len - 48) // 16, n)
+    _check_i32(n, out_len=out_len, status=status, key_idx=key_idx)
+    lib = _native.load()
+    _native.check(lib.rt_decrypt_interleaved(ks.handle, _p(tok), tok_len, _p(key_idx), _p(pt), _p(out_len),
+                                             _p(status), n, _stream(stream, tok.device)))
+
+
 def verify(ks: KeySet, tok, tok_off, tok_len, status, key_idx=None, stream=None):
     """Token.verify_hmac (Token.py:77-84) over device buffers, no AES: token
     i is tok[tok_off[i] : +tok_len[i]] (int64 / int32); status (n,) int32

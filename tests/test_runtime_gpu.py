@@ -460,3 +460,50 @@ def test_device_keyset_on_side_stream_after_current_stream_fill(rt):
         for i in range(0, n, 61):
             assert t[i].tobytes() == oracle.encrypt(keys[kidx[i]].tobytes(), iv[i].tobytes(), pt[i].tobytes()), trial
         del junk
+
+
+def test_counter_ring_eight_threads_ragged_launches(rt):
+    """the chunk-counter ring holds no lock across a
+    launch.  Eight host threads, each on its own torch stream, issue ragged
+    launches (the dynamic chunk loop: one slot per launch) of their own
+    batches, 1-key and per-packet-key, with the output zeroed before every
+    launch; every output must equal the batch's reference (a slot handed to
+    two launches at once, or zeroed under a running one, would skip or repeat
+    chunks and leave zeros).  Prints launches/s for 1 and 8 threads."""
+    import threading
+    import time
+    import torch
+    from reticulum_amd import device
+    base = [_ragged_case(rt, 262_211, 16, 1, 11), _ragged_case(rt, 196_999, 32, 77, 12)]   # > 1 pass, ragged
+    n_thr, iters = 8, 150
+    streams = [torch.cuda.Stream() for _ in range(n_thr)]
+    outs = [torch.empty_like(base[t % 2][4]) for t in range(n_thr)]
+    bad = [torch.zeros((), dtype=torch.int64, device="cuda") for _ in range(n_thr)]
+    errors = []
+
+    def worker(t, k):
+        try:
+            ks, pt, iv, ki, ref = base[t % 2]
+            with torch.cuda.stream(streams[t]):
+                for _ in range(k):
+                    outs[t].zero_()
+                    device.encrypt_uniform(ks, pt, pt.shape[1], iv, outs[t], key_idx=ki, stream=streams[t])
+                    bad[t] += (outs[t] != ref).any(dim=1).sum()
+        except Exception as e:   # noqa: BLE001 (reported below)
+            errors.append(repr(e))
+
+    rates = {}
+    for nt in (1, n_thr):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=worker, args=(t, iters)) for t in range(nt)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        torch.cuda.synchronize()
+        rates[nt] = nt * iters / (time.perf_counter() - t0)
+    assert not errors, errors
+    assert [int(b) for b in bad] == [0] * n_thr
+    print(f"\nragged launches/s (launch + zero + compare per iteration): 1 thread {rates[1]:.0f}, "
+          f"{n_thr} threads {rates[n_thr]:.0f}")

@@ -57,6 +57,8 @@ def main():
     for path in args.libs:
         lib = ctypes.CDLL(os.path.abspath(path))
         for name, res, argt in _native.SIGNATURES:
+            if not hasattr(lib, name):        # an older build of the library: entry points added since
+                continue
             f = getattr(lib, name)
             f.restype, f.argtypes = res, argt
         ctx = lib.rt_create(0)

@@ -333,13 +333,8 @@ def main():
 
     # PCIe-inclusive (host buffers, pinned) rate for DESIGN.md: every rank at
     # once on its own shard, over its own PCIe link (the node's host-origin rate)
-    e2e = None
-    if args.e2e:
-        if world > 1:
-            e2e = e2e_rate(ks, pt, iv, L, tl, n, stream, sync_all=dist.barrier,
-                           reduce_max=lambda v: _reduce_max(v, dev), world=world)
-        else:
-            e2e = e2e_rate(ks, pt, iv, L, tl, n, stream)
+    # (N > 1: below, after the headline line exists, under a deadline)
+    e2e = e2e_rate(ks, pt, iv, L, tl, n, stream) if args.e2e and world == 1 else None
 
     lib = _native.load()
     n_cu = lib.rt_num_cus(_native.context(local))
@@ -432,6 +427,16 @@ def main():
     # point-to-point transfer) makes rank 0 print the line with the error and
     # every rank exit, before the process group's own 300 s timeout would
     # abort the job without a line.
+    if world > 1 and args.e2e:
+        # every rank's host-origin path at once; a stuck barrier or reduction
+        # here must not cost the headline line either
+        guard = _LineGuard(line if rank == 0 else None, 120.0, field="e2e_pcie", what="host-origin pass")
+        try:
+            line["e2e_pcie"] = e2e_rate(ks, pt, iv, L, tl, n, stream, sync_all=dist.barrier,
+                                        reduce_max=lambda v: _reduce_max(v, dev), world=world)
+        except Exception as e:  # reported, never fatal for the headline line
+            line["e2e_pcie"] = {"error": f"{type(e).__name__}: {e}"}
+        guard.finish()
     if world > 1 and os.environ.get("RNSTOK_BENCH_SHARDED", "1") != "0":
         guard = _LineGuard(line if rank == 0 else None, args.sharded_timeout)
         try:
@@ -495,13 +500,15 @@ def _cpu_phase(line, args, L, rank):
 
 
 class _LineGuard:
-    """Deadline for the optional sharded pass of an N > 1 run.  On expiry
-    rank 0 prints the headline line (sharded_c4 carrying the error) and every
-    rank leaves with status 0; finish() cancels it."""
+    """Deadline for an optional phase of an N > 1 run (the sharded pass, the
+    host-origin pass).  On expiry rank 0 prints the headline line (``field``
+    carrying the error) and every rank leaves with status 0; finish() cancels
+    it."""
 
-    def __init__(self, line, seconds):
+    def __init__(self, line, seconds, field="sharded_c4", what="sharded pass"):
         import threading
         self.line, self.lock, self.done = line, threading.Lock(), False
+        self.field, self.what = field, what
         self.timer = threading.Timer(seconds, self._expire, args=(seconds,))
         self.timer.daemon = True
         self.timer.start()
@@ -512,8 +519,8 @@ class _LineGuard:
                 return
             self.done = True
             if self.line is not None:
-                prev = self.line.get("sharded_c4")
-                self.line["sharded_c4"] = {"error": f"sharded pass unfinished after {seconds} s", "partial": prev}
+                prev = self.line.get(self.field)
+                self.line[self.field] = {"error": f"{self.what} unfinished after {seconds} s", "partial": prev}
                 print(json.dumps(self.line), flush=True)
             sys.stderr.flush()
             os._exit(0)
@@ -678,7 +685,7 @@ def sharded_bench(cfg, args, world, rank, local, reps=3):
         # the same pass with the legs overlapped (shard.sharded_call_pipelined):
         # its output must equal the serial pass's
         piped_s = piped_ok = None
-        if dist_on and world > 1 and args.sharded_chunks > 0:
+        if dist_on and world > 1 and getattr(args, "sharded_chunks", 0) > 0:
             cap = tok_lengths if name == "encrypt" else (lambda x: (x - 48).clamp(min=0))
             out_specs = [] if name == "encrypt" else [(torch.int32, 0), (torch.int32, 0)]
             best = float("inf")
@@ -747,7 +754,7 @@ def sharded_bench(cfg, args, world, rank, local, reps=3):
         "gather_ms": total["gather_s"] * 1e3, "key_broadcast_setup_ms": keys_ms, "scaling": "strong", "ok": ok,
         "pipelined_ms": total.get("pipelined_s", 0.0) * 1e3 or None,
         "pipelined_end_to_end_packets_s": pkts / total["pipelined_s"] if total.get("pipelined_s") else None,
-        "pipelined_note": (f"shard.sharded_call_pipelined, {args.sharded_chunks} chunks per rank: the inputs of chunk "
+        "pipelined_note": (f"shard.sharded_call_pipelined, {getattr(args, 'sharded_chunks', 0)} chunks per rank: the inputs of chunk "
                            f"k and the outputs of chunk k-2 move in one grouped RCCL batch while chunk k-1 computes; "
                            f"best of {reps} passes, max over ranks; output checked equal to the serial pass's"),
         "data": "synthetic random plaintext, IVs and keys generated on rank 0's device",

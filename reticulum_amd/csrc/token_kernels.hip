@@ -462,6 +462,8 @@ __global__ __launch_bounds__(256) void k_encrypt_long(EncArgs a) {
 // (16 per wave) and drop each quad of ciphertext into a two-slot LDS ring;
 // waves 8-9 hash the previous quad of the same tokens, one token per lane,
 // one barrier per quad step.  Single key, uniform lengths.
+// Hashing waves: 4 (one per SIMD, 32 tokens each) measured 8 % slower than 2
+// on the c4 shard (profiles/r03g_long4_ab.txt).
 #ifndef RNSTOK_L4_HASH_WAVES
 #define RNSTOK_L4_HASH_WAVES 2
 #endif
@@ -470,17 +472,19 @@ constexpr uint32_t L4_THREADS = 64u * (L4_AES_WAVES + L4_HASH_WAVES), L4_HASH_TO
 static_assert(L4_HASH_TOK <= 64u && L4_TOK % L4_HASH_WAVES == 0u, "one token per hashing lane");
 
 // Ring layout: token t's quad (4 blocks x 16 B) at t*64 B, block i in 16-B
-// unit i ^ l4_swz(t).  Without the swizzle the AES lanes' 4-B stores (lanes of
-// 8 consecutive tokens x 4 columns) met 4-way and the hashing lanes' 16-B
+// unit i ^ l4_swz(t).  Unswizzled, the AES lanes' 4-B stores (lanes of 8
+// consecutive tokens x 4 columns) meet 4-way and the hashing lanes' 16-B
 // reads (one token per lane) 4-way bank conflicts (7 % of the kernel's LDS
-// cycles, profiles/r02e_c4s8_pmc_summary.txt); with it both are conflict-free
-// for ds_write_b32's 2 x 32 and ds_read_b128's 4 x 16 lane groups
-// (MI355X_MICROARCH.md LDS table; exhaustive check in DESIGN.md §4.2).
+// cycles, profiles/r02e_c4s8_pmc_summary.txt).  RNSTOK_L4_SWIZZLE makes both
+// conflict-free for ds_write_b32's 2 x 32 and ds_read_b128's 4 x 16 lane
+// groups (MI355X_MICROARCH.md LDS table; exhaustive check in DESIGN.md §4.2),
+// but measured 1.2 % slower on the c4 shard (1.001 vs 0.989 ms,
+// profiles/r03g_long4_ab.txt): the LDS pipe is not what bounds this kernel.
 __device__ __forceinline__ uint32_t l4_swz(uint32_t t) {
-#ifndef RNSTOK_L4_NO_SWIZZLE
+#ifdef RNSTOK_L4_SWIZZLE
     return ((t >> 1) ^ (t >> 2)) & 3u;
 #else
-    return 0u;
+    return 0u * t;
 #endif
 }
 constexpr uint32_t L4_RING = LDS_ENC_BYTES;                              // after the table image
@@ -534,10 +538,11 @@ __device__ __forceinline__ uint32_t enc_block4(uint32_t s, const uint32_t *rk, c
         // bound, and this is a shorter dependent path than the three
         // v_xor_b32_dpp in a row the compiler folds the plain XORs into
         // (c4 shard encrypt 1.044 -> 0.992 ms, A/B)
-#ifndef RNSTOK_L4_XOR_CHAIN3
-        // two of the moves carry an XOR (v_xor_b32 with a DPP source: the
-        // round key and this lane's own term ride on them), so the new column
-        // is ONE xor3 after the moves instead of two in a row
+#ifdef RNSTOK_L4_FOLD
+        // experiment (round 3): two of the moves carry an XOR (v_xor_b32 with
+        // a DPP source: the round key and this lane's own term ride on them),
+        // one xor3 after the moves instead of two in a row.  3.8 % slower on
+        // the c4 shard (1.026 vs 0.989 ms, profiles/r03g_long4_ab.txt).
         uint32_t x1 = quad_rot<1>(u1) ^ u0, x2 = quad_rot<2>(u2) ^ rk[r], x3 = quad_rot<3>(u3);
         asm volatile("" : "+v"(x1), "+v"(x2), "+v"(x3));
         s = xor3(x1, x2, x3);

@@ -80,3 +80,84 @@ def test_cpu_openssl_row_without_library(tmp_path, monkeypatch):
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))     # no tools/libcpu_openssl.so there
     assert bench.cpu_openssl(1.0, 1, 500) is None
     assert bench.cpu_openssl(0.0, 1, 500) is None
+
+
+def _cpu_phase_worker(rank, world, port, q):
+    import argparse
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, ROOT)
+    import bench
+    import time
+    line = {"value": 1.0, "cpu_baseline": None, "cpu_openssl": None}
+    t0 = time.perf_counter()
+    bench._cpu_phase(line, argparse.Namespace(cpu_seconds=0.5, cpu_workers=2), 500, rank)
+    q.put((rank, line["cpu_baseline"], time.perf_counter() - t0))
+    dist.destroy_process_group()
+
+
+def test_cpu_baseline_phase_at_n_gt_1():
+    """at N > 1 rank 0 times the CPU baseline after the
+    GPU phases while the other ranks wait on the rendezvous store; every
+    rank leaves only when rank 0 is done, and the line carries the baseline."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    procs = [ctx.Process(target=_cpu_phase_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    got = {r: (cpu, dt) for r, cpu, dt in (q.get() for _ in range(2))}
+    cpu0 = got[0][0]
+    assert cpu0["kind"] == "port" and cpu0["value"] > 0 and cpu0["cores"] == 2 and "rank 0" in cpu0["note"]
+    assert got[1][0] is None and got[1][1] >= 0.5          # rank 1 waited for rank 0's timed phase
+
+
+def test_guard_names_its_phase():
+    """The host-origin pass of an N > 1 run has its own deadline: on expiry
+    the line carries the error under e2e_pcie, the headline intact."""
+    p = _run("import bench, time\n"
+             "line = {'metric': 'm', 'value': 3.0, 'e2e_pcie': None, 'sharded_c4': None}\n"
+             "g = bench._LineGuard(line, 0.3, field='e2e_pcie', what='host-origin pass')\n"
+             "time.sleep(20)\n")
+    assert p.returncode == 0, p.stderr
+    rec = json.loads(p.stdout.strip())
+    assert rec["value"] == 3.0 and rec["sharded_c4"] is None
+    assert rec["e2e_pcie"]["error"] == "host-origin pass unfinished after 0.3 s"
+
+
+def test_committed_n_gt_1_lines_carry_every_north_star_number():
+    """VERDICT r02 next #2, checked on the committed rehearsal lines of
+    bench.py's N > 1 path (RNSTOK_BENCH_REHEARSE=1: every rank on one GPU over
+    gloo, 2 and 4 ranks; not measurements): the weak-scaling headline, the
+    node's host-origin aggregate, the CPU baseline timed in the same run, and
+    the sharded c4 pass with its serial legs and the pipelined pass, whose
+    output equals the serial pass's."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r03*_rehearse_n*_gloo.json")))
+    assert len(paths) >= 2
+    for p in paths:
+        with open(p) as f:
+            rec = json.loads(f.read().strip().splitlines()[-1])
+        n = rec["n_gpus"]
+        assert n >= 2 and rec["value"] > 0 and rec["scaling"] == "weak"
+        agg = rec["e2e_pcie"]["aggregate"]
+        assert agg["ranks"] == n
+        for leg in ("serial", "pipelined"):
+            assert agg[leg]["ok_all"] is True and agg[leg]["encrypt_packets_s"] > 0 and agg[leg]["decrypt_packets_s"] > 0
+        cpu = rec["cpu_baseline"]
+        assert cpu["kind"] == "port" and cpu["value"] > 0 and cpu["cores"] >= 1
+        sc = rec["sharded_c4"]
+        assert sc["ok"] is True and sc["n_gpus"] == n
+        ph = sc["phases"]["encrypt"]
+        assert min(ph["scatter_ms"], ph["compute_ms"], ph["gather_ms"], ph["pipelined_ms"]) > 0
+        assert ph["pipelined_equals_serial"] is True and ph["pipelined_chunks"] >= 1

@@ -79,9 +79,11 @@ def parse():
                     help="N > 1: chunks per rank of the pipelined sharded pass (0 disables it)")
     ap.add_argument("--sharded-timeout", type=float, default=150.0,
                     help="N > 1: seconds allowed for the sharded c4 pass after the headline")
-    ap.add_argument("--layout", choices=["rows", "interleaved"], default="rows",
-                    help="HBM layout of the c2/c3 batch: packed rows (the reference's byte strings) or the "
-                         "unit-interleaved device layout (rt_encrypt_interleaved)")
+    ap.add_argument("--layout", choices=["rows", "interleaved"], default="interleaved",
+                    help="HBM layout the headline is timed on: the unit-interleaved device layout "
+                         "(rt_encrypt_interleaved, coalesced) or packed rows (the reference's byte strings); "
+                         "the other layout is timed right after it")
+    ap.add_argument("--one-layout", action="store_true", help="time only --layout")
     ap.add_argument("--e2e", action="store_true", default=True, help="also time the PCIe-inclusive path")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false")
     return ap.parse_args()
@@ -273,63 +275,84 @@ def main():
         key_idx = torch.randint(0, args.keys, (n,), dtype=torch.int32, device=dev, generator=g)
     stream = torch.cuda.current_stream()
 
-    ilv = args.layout == "interleaved"
-    if ilv:
-        # the unit-interleaved device layout (rt_encrypt_interleaved): the same
-        # packets, 16-B unit u of packet p at 16*(u*n + p)
-        pt_u = device.interleave(pt, L)
-        tok_u = torch.empty((tl // 16, n, 16), dtype=torch.uint8, device=dev)
-        back_u = torch.empty(((tl - 48) // 16, n, 16), dtype=torch.uint8, device=dev)
+    # Both HBM layouts of the same packets: packed rows (pt row i = packet i,
+    # the reference's byte strings) and the unit-interleaved device layout
+    # (rt_encrypt_interleaved: 16-B unit u of packet p at 16*(u*n + p), every
+    # wave load/store one contiguous KiB: north_star's "coalesced HBM loads
+    # across the packet batch").  Tokens and plaintexts are identical in both
+    # (checked below); --layout picks the one the headline value is timed on,
+    # the other is timed right after it in the same run.
+    pt_u = device.interleave(pt, L)
+    tok_u = torch.empty((tl // 16, n, 16), dtype=torch.uint8, device=dev)
+    back_u = torch.empty(((tl - 48) // 16, n, 16), dtype=torch.uint8, device=dev)
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        if ilv:
-            device.encrypt_interleaved(ks, pt_u, L, iv, tok_u, key_idx=key_idx, stream=stream)
-        else:
-            device.encrypt_uniform(ks, pt, L, iv, tok, key_idx=key_idx, stream=stream)
-        if ev is not None:
-            ev[1].record(stream)
-        if ilv:
-            device.decrypt_interleaved(ks, tok_u, tl, back_u, out_len, status, key_idx=key_idx, stream=stream)
-        else:
-            device.decrypt_uniform(ks, tok, tl, back, out_len, status, key_idx=key_idx, stream=stream)
-        if ev is not None:
-            ev[2].record(stream)
+    def make_step(layout):
+        ilv = layout == "interleaved"
 
+        def step(ev=None):
+            if ev is not None:
+                ev[0].record(stream)
+            if ilv:
+                device.encrypt_interleaved(ks, pt_u, L, iv, tok_u, key_idx=key_idx, stream=stream)
+            else:
+                device.encrypt_uniform(ks, pt, L, iv, tok, key_idx=key_idx, stream=stream)
+            if ev is not None:
+                ev[1].record(stream)
+            if ilv:
+                device.decrypt_interleaved(ks, tok_u, tl, back_u, out_len, status, key_idx=key_idx, stream=stream)
+            else:
+                device.decrypt_uniform(ks, tok, tl, back, out_len, status, key_idx=key_idx, stream=stream)
+            if ev is not None:
+                ev[2].record(stream)
+        return step
+
+    layouts = [args.layout] + ([] if args.one_layout else [x for x in ("interleaved", "rows") if x != args.layout])
+    steps = {lay: make_step(lay) for lay in layouts}
     # correctness gate on the benchmarked data (size-independent properties),
     # before the warmup so that nothing idles the GPU between warmup and timing
-    step()
-    torch.cuda.synchronize()
-    if ilv:
-        back = device.deinterleave(back_u, tl - 48)
-    ok = bool((status == 0).all()) and bool((out_len == L).all()) and torch.equal(back[:, :L], pt)
-    if not ok:
-        raise SystemExit("bench: round trip failed on the benchmark batch")
+    for lay in layouts:
+        steps[lay]()
+        torch.cuda.synchronize()
+        got = device.deinterleave(back_u, tl - 48) if lay == "interleaved" else back
+        ok = bool((status == 0).all()) and bool((out_len == L).all()) and torch.equal(got[:, :L], pt)
+        if not ok:
+            raise SystemExit(f"bench: round trip failed on the benchmark batch ({lay} layout)")
+    if len(layouts) == 2 and not torch.equal(device.deinterleave(tok_u, tl), tok):
+        raise SystemExit("bench: the two layouts' tokens differ")
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    warm_steps, warm_s = warmup(step, stream, args.warmup, args.warmup_seconds)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(evs[k])
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    elapsed = t1 - t0
-    enc_ms = sorted(e[0].elapsed_time(e[1]) for e in evs)
-    dec_ms = sorted(e[1].elapsed_time(e[2]) for e in evs)
-    enc_avg = sum(enc_ms) / len(enc_ms)
-    dec_avg = sum(dec_ms) / len(dec_ms)
-    if world > 1:
-        t = torch.tensor([elapsed, enc_avg, dec_avg], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, enc_avg, dec_avg = t.tolist()
+    def timed(step):
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        if world > 1:
+            dist.barrier()
+        warm = warmup(step, stream, args.warmup, args.warmup_seconds)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(evs[k])
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        el = t1 - t0
+        e_ms = sorted(e[0].elapsed_time(e[1]) for e in evs)
+        d_ms = sorted(e[1].elapsed_time(e[2]) for e in evs)
+        e_avg, d_avg = sum(e_ms) / len(e_ms), sum(d_ms) / len(d_ms)
+        if world > 1:
+            t = torch.tensor([el, e_avg, d_avg], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el, e_avg, d_avg = t.tolist()
+        return el, e_avg, d_avg, e_ms, d_ms, warm
+
+    elapsed, enc_avg, dec_avg, enc_ms, dec_ms, (warm_steps, warm_s) = timed(steps[layouts[0]])
+    other = None
+    if len(layouts) == 2:
+        el2, e2, d2, _, _, _ = timed(steps[layouts[1]])
+        other = {"layout": layouts[1], "value": n * world * args.steps / el2, "ms_per_step": el2 / args.steps * 1e3,
+                 "encrypt_ms": e2, "decrypt_ms": d2,
+                 "note": "the same packets in the other HBM layout, timed right after the headline in this run "
+                         "(same warmup rule); tokens identical to the headline layout's (checked)"}
 
     # PCIe-inclusive (host buffers, pinned) rate for DESIGN.md: every rank at
     # once on its own shard, over its own PCIe link (the node's host-origin rate)
@@ -378,6 +401,11 @@ def main():
                    if (n == 1 << 20 and L == 500) else f"{n} x {L} B packets per GPU, {args.keys} key(s)",
                    "packets_per_gpu": n, "plaintext_bytes": L, "token_bytes": tl, "keys": args.keys,
                    "row_strides": {"plaintext": ps, "token": ts}, "layout": args.layout,
+                   "layout_note": ("unit-interleaved: 16-B unit u of packet p at 16*(u*n + p) (rt_encrypt_interleaved; "
+                                   "coalesced HBM loads across the batch); the packed-row layout's numbers are under "
+                                   "other_layout" if args.layout == "interleaved" else
+                                   "packed rows (packet i at i*stride); the interleaved layout's numbers are under "
+                                   "other_layout"),
                    "step": "encrypt+MAC then verify+decrypt of the same batch", "parallelism": f"shard{world}"},
         "kernels": {
             "encrypt": {"ms": enc_avg, "ms_median": enc_ms[len(enc_ms) // 2], "packets_s": n / (enc_avg * 1e-3),
@@ -416,6 +444,7 @@ def main():
                              "kernel's own compute core timed from registers (tools/floor_probe.hip); DESIGN.md §4.5"},
         "cpu_baseline": cpu,
         "cpu_openssl": cpu_ssl,
+        "other_layout": other,
         "e2e_pcie": e2e,
         "sharded_c4": None,
     }

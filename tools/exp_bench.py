@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--probe", action="store_true", help="timing probes: skip the round-trip assertion")
     ap.add_argument("--kidx", choices=["random", "zero", "seq", "sorted"], default="random",
                     help="per-packet key pattern (with --keys > 1)")
+    ap.add_argument("--ilv", action="store_true", help="the unit-interleaved layout (rt_encrypt_interleaved)")
     ap.add_argument("--packed", type=int, default=-1,
                     help="variable lengths drawn from [PACKED, length] through rt_encrypt/rt_decrypt (packed entry)")
     args = ap.parse_args()
@@ -80,10 +81,17 @@ def main():
         p_off, t_off, b_off = rows * L, rows * tl, rows * (tl - 48)
         t_len = (16 + 16 * (lens // 16 + 1) + 32).to(torch.int32)
 
+    if args.ilv:
+        from reticulum_amd import device as _dev
+        pt_u = _dev.interleave(pt, L)
+
     def run(v, ev=None):
         if ev:
             ev[0].record(s)
-        if packed:
+        if args.ilv:
+            rc = v["lib"].rt_encrypt_interleaved(v["ks"], pt_u.data_ptr(), L, kp, iv.data_ptr(), v["tok"].data_ptr(),
+                                                 n, sp)
+        elif packed:
             rc = v["lib"].rt_encrypt(v["ks"], pt_buf.data_ptr(), p_off.data_ptr(), lens.data_ptr(), kp, iv.data_ptr(),
                                      v["tok"].data_ptr(), t_off.data_ptr(), n, sp)
         else:
@@ -92,7 +100,10 @@ def main():
         assert rc == 0
         if ev:
             ev[1].record(s)
-        if packed:
+        if args.ilv:
+            rc = v["lib"].rt_decrypt_interleaved(v["ks"], v["tok"].data_ptr(), tl, kp, v["back"].data_ptr(),
+                                                 v["ol"].data_ptr(), v["st"].data_ptr(), n, sp)
+        elif packed:
             rc = v["lib"].rt_decrypt(v["ks"], v["tok"].data_ptr(), t_off.data_ptr(), t_len.data_ptr(), kp,
                                      v["back"].data_ptr(), b_off.data_ptr(), v["ol"].data_ptr(), v["st"].data_ptr(), n, sp)
         else:
@@ -111,6 +122,9 @@ def main():
             ok = bool((v["st"] == 0).all()) and torch.equal(v["ol"], lens)
             for i in range(0, n, max(1, n // 64)):
                 ok = ok and torch.equal(v["back"][i, :int(lens[i])], pt[i, :int(lens[i])])
+        elif args.ilv:
+            back = _dev.deinterleave(v["back"].view((tl - 48) // 16, n, 16), tl - 48)
+            ok = bool((v["st"] == 0).all()) and torch.equal(back[:, :L], pt)
         else:
             ok = bool((v["st"] == 0).all()) and torch.equal(v["back"][:, :L], pt)
         if packed:     # token bytes only (rows are wider than their tokens)

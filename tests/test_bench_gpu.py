@@ -16,5 +16,21 @@ def test_sharded_config_world1(cfg, packets):
     rep = bench.sharded_bench(cfg, args, world=1, rank=0, local=0, reps=1)
     assert rep["ok"] is True
     assert rep["config"]["packets"] == packets
-    assert set(rep["phases"]) == ({"encrypt"} if cfg == "c4" else {"encrypt", "decrypt"})
+    assert set(rep["phases"]) == {"encrypt", "decrypt"}
+    # c4: every segment encrypted, then its token decrypted;
+    # c5: half and half
+    per = packets if cfg == "c4" else packets // 2
+    assert rep["phases"]["encrypt"]["packets"] == per
+    assert rep["phases"]["decrypt"]["packets"] == packets - (0 if cfg == "c4" else per)
     assert rep["value"] > 0 and rep["compute_ms"] > 0
+
+
+def test_c3_key_setup_times():
+    """the per-key setup timed apart from the steps, from a
+    host table and from a table already in HBM."""
+    import numpy as np
+    import torch
+    import bench
+    keys = np.random.default_rng(3).integers(0, 256, (4096, 64), dtype=np.uint8)
+    r = bench.key_setup_times(keys, 0, torch.device("cuda", 0), reps=2)
+    assert r["keys"] == 4096 and r["host_ms"] > 0 and r["device_ms"] > 0 and r["keys_per_s_device"] > 0

@@ -977,6 +977,12 @@ def e2e_rate(ks, pt_dev, iv_dev, L, tl, n, stream, reps=3, chunks=32, n_streams=
     * pipelined: the batch cut into `chunks` slices issued round-robin on
       `n_streams` streams, so one slice's H2D, another's kernel and a third's
       D2H overlap (PCIe is full duplex).
+    H2D runs on the copy engine (torch copy_), D2H as GPU stores into the
+    pinned buffer (device.copy_to_host): on MI355X the copy engine does D2H at
+    30 GB/s and shares 57 GB/s between the two directions, the stores do
+    54 GB/s and 87 GB/s beside a copy-engine H2D (profiles/r03n_pcie_probe.json).
+    ``pipelined_copy_engine`` times the same slices with both directions on
+    the copy engine (the round-1/2 path), for comparison.
     Best of `reps`; the round trip is checked on the host copies.
 
     N > 1 (VERDICT r02 missing #1): every rank runs this at once on its own
@@ -1003,40 +1009,48 @@ def e2e_rate(ks, pt_dev, iv_dev, L, tl, n, stream, reps=3, chunks=32, n_streams=
         step = -(-n // parts)
         return [(a, min(a + step, n)) for a in range(0, n, step)]
 
-    def enc(parts):
+    def d2h(dst, src, s, engine):
+        if engine:
+            dst.copy_(src, non_blocking=True)
+        else:
+            device.copy_to_host(dst, src, stream=s)
+
+    def enc(parts, engine=False):
         for k, (a, b) in enumerate(slices(parts)):
             s = stream if parts == 1 else side[k % n_streams]
             with torch.cuda.stream(s):
                 pt_d[a:b].copy_(pt_h[a:b], non_blocking=True)
                 iv_d[a:b].copy_(iv_h[a:b], non_blocking=True)
                 device.encrypt_uniform(ks, pt_d[a:b], L, iv_d[a:b], tok_d[a:b], stream=s)
-                tok_h[a:b].copy_(tok_d[a:b], non_blocking=True)
+                d2h(tok_h[a:b], tok_d[a:b], s, engine)
 
-    def dec(parts):
+    def dec(parts, engine=False):
         for k, (a, b) in enumerate(slices(parts)):
             s = stream if parts == 1 else side[k % n_streams]
             with torch.cuda.stream(s):
                 tok_d[a:b].copy_(tok_h[a:b], non_blocking=True)
                 device.decrypt_uniform(ks, tok_d[a:b], tl, back_d[a:b], ol[a:b], st[a:b], stream=s)
-                back_h[a:b].copy_(back_d[a:b], non_blocking=True)
+                d2h(back_h[a:b], back_d[a:b], s, engine)
 
-    def timed(fn, parts):
+    def timed(fn, parts, engine):
         own, slowest = [], []
         for _ in range(reps):
             torch.cuda.synchronize()
             if sync_all is not None:
                 sync_all()
             t0 = time.perf_counter()
-            fn(parts)
+            fn(parts, engine)
             torch.cuda.synchronize()
             own.append(time.perf_counter() - t0)
         slowest = reduce_max(own) if reduce_max is not None else own
         return min(own), min(slowest)
 
     res, agg = {}, {}
-    for name, parts in (("serial", 1), ("pipelined", chunks)):
+    for name, parts, engine in (("serial", 1, False), ("pipelined", chunks, False),
+                                ("pipelined_copy_engine", chunks, True)):
         back_h.zero_()
-        (te, te_all), (td, td_all) = timed(enc, parts), timed(dec, parts)
+        tok_h.zero_()
+        (te, te_all), (td, td_all) = timed(enc, parts, engine), timed(dec, parts, engine)
         ok = bool((st == 0).all()) and torch.equal(back_h[:, :L], pt_h)
         res[name] = {"encrypt_packets_s": n / te, "decrypt_packets_s": n / td, "roundtrip_packets_s": n / (te + td),
                      "encrypt_gib_s": n * L / te / 2**30, "decrypt_gib_s": n * L / td / 2**30,
@@ -1046,9 +1060,10 @@ def e2e_rate(ks, pt_dev, iv_dev, L, tl, n, stream, reps=3, chunks=32, n_streams=
                      "encrypt_gib_s": world * n * L / te_all / 2**30, "decrypt_gib_s": world * n * L / td_all / 2**30,
                      "ok_all": ok}
     res["note"] = (f"pinned host buffers; serial = H2D + kernel + D2H on one stream; pipelined = {chunks} slices "
-                   f"round-robin on {n_streams} streams; best of {reps}")
+                   f"round-robin on {n_streams} streams; H2D on the copy engine, D2H as GPU stores into the pinned "
+                   f"buffer (pipelined_copy_engine: D2H on the copy engine too); best of {reps}")
     if world > 1:
-        flags = reduce_max([0.0 if (res["serial"]["ok"] and res["pipelined"]["ok"]) else 1.0])
+        flags = reduce_max([0.0 if all(res[k]["ok"] for k in agg) else 1.0])
         for name in agg:
             agg[name]["ok_all"] = flags[0] == 0.0
         agg["ranks"] = world

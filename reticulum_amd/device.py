@@ -438,3 +438,28 @@ def pack_headers(flags, hops, destination_hash, context, out, out_off, transport
     _native.check(lib.rt_packet_pack_headers(_ctx_of(out), _p(flags), _p(hops), _p(transport_id),
                                              _p(destination_hash), _p(context), _p(out), _p(out_off), n,
                                              _stream(stream, out.device)))
+
+
+# ------------------------------------------------------- host-origin path --
+
+def copy_to_host(dst, src, stream=None):
+    """Enqueue ``dst.copy_(src)`` for a device tensor ``src`` and a host tensor
+    ``dst`` of the same size, both contiguous, through rt_memcpy_d2h: a pinned
+    ``dst`` is written by GPU stores into the mapped host buffer
+    (copy_kernels.hip; 54 GB/s alone and 87 GB/s beside a copy-engine H2D on
+    MI355X, against 30 GB/s for the copy engine's D2H,
+    profiles/r03n_pcie_probe.json), a pageable one by hipMemcpyAsync.  Like
+    ``copy_(non_blocking=True)`` nothing is synchronised: ``dst`` is valid
+    once ``stream`` (default: the current stream of src's GPU) has run."""
+    if not src.is_cuda or dst.is_cuda:
+        raise ValueError("copy_to_host copies a device tensor into a host tensor")
+    if not src.is_contiguous() or not dst.is_contiguous():
+        raise ValueError("copy_to_host needs contiguous tensors")
+    nbytes = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() != nbytes:
+        raise ValueError("copy_to_host: size mismatch")
+    if nbytes == 0:
+        return
+    lib = _native.load()
+    _native.check(lib.rt_memcpy_d2h(_ctx_of(src), dst.data_ptr(), src.data_ptr(), nbytes,
+                                    _stream(stream, src.device)))

@@ -7,6 +7,6 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p $ROOT/build_exp/$NAME
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -w "$@" -shared -o $ROOT/build_exp/$NAME/librnstok.so \
   $ROOT/reticulum_amd/csrc/token_kernels.hip $ROOT/reticulum_amd/csrc/hkdf_kernels.hip $ROOT/reticulum_amd/csrc/resource_kernels.hip \
-  $ROOT/reticulum_amd/csrc/wire_kernels.hip \
+  $ROOT/reticulum_amd/csrc/wire_kernels.hip $(ls $ROOT/reticulum_amd/csrc/copy_kernels.hip 2>/dev/null) \
   $ROOT/reticulum_amd/csrc/token_capi.hip
 echo built build_exp/$NAME

@@ -1,5 +1,5 @@
 """Sweep of the PCIe-inclusive (pinned host memory in and out) pipeline shape:
-slices x streams, c2 batch (2^20 x 500 B, one key).  Prints one JSON line per
+slices x streams x D2H mechanism (GPU stores / copy engine), c2 batch (2^20 x 500 B, one key).  Prints one JSON line per
 shape with encrypt / decrypt packets/s (bench.e2e_rate, best of 3).
 
   python tools/e2e_sweep.py [--chunks 8,16,32,64] [--streams 2,3,4,8]
@@ -32,10 +32,12 @@ def main():
     stream = torch.cuda.current_stream()
     for c in map(int, args.chunks.split(",")):
         for s in map(int, args.streams.split(",")):
-            r = bench.e2e_rate(ks, pt, iv, L, tl, n, stream, chunks=c, n_streams=s)["pipelined"]
-            print(json.dumps({"chunks": c, "streams": s, "enc_Mpkt_s": r["encrypt_packets_s"] / 1e6,
-                              "dec_Mpkt_s": r["decrypt_packets_s"] / 1e6, "pcie_gb_s": r["encrypt_pcie_gb_s"],
-                              "ok": r["ok"]}), flush=True)
+            res = bench.e2e_rate(ks, pt, iv, L, tl, n, stream, chunks=c, n_streams=s)
+            for d2h, key in (("stores", "pipelined"), ("copy_engine", "pipelined_copy_engine")):
+                r = res[key]
+                print(json.dumps({"chunks": c, "streams": s, "d2h": d2h, "enc_Mpkt_s": r["encrypt_packets_s"] / 1e6,
+                                  "dec_Mpkt_s": r["decrypt_packets_s"] / 1e6, "pcie_gb_s": r["encrypt_pcie_gb_s"],
+                                  "ok": r["ok"]}), flush=True)
 
 
 if __name__ == "__main__":

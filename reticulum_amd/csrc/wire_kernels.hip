@@ -87,18 +87,6 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_add(uint64_t *out, const ui
 
 // ------------------------------------------------------- byte helpers --
 
-// little-endian word of p[i, i+4), bytes at or past `end` read as 0
-__device__ __forceinline__ uint32_t ld4_upto(const uint8_t *p, uint64_t i, uint64_t end) {
-    if (i + 4 <= end) {
-        uint32_t v;
-        __builtin_memcpy(&v, p + i, 4);
-        return v;
-    }
-    uint32_t v = 0;
-    for (uint32_t k = 0; k < 4; ++k)
-        if (i + k < end) v |= (uint32_t)p[i + k] << (8 * k);
-    return v;
-}
 // 0x80 in every byte of x equal to the byte replicated in c4 (exact: no borrow crosses bytes)
 __device__ __forceinline__ uint32_t eqbytes(uint32_t x, uint32_t c4) {
     const uint32_t t = x ^ c4;
@@ -134,7 +122,22 @@ __device__ __forceinline__ uint32_t row_incl_scan16(uint32_t x) {
     x += dpp<0x118>(x);     // row_shr:8
     return x;
 }
-// 16 bytes of p[i, i+16), bytes at or past `end` read as 0
+// little-endian word of p[i, i+4), bytes at or past `end` read as 0
+__device__ __forceinline__ uint32_t ld4_upto(const uint8_t *p, uint64_t i, uint64_t end) {
+    if (i + 4 <= end) {
+        uint32_t v;
+        __builtin_memcpy(&v, p + i, 4);
+        return v;
+    }
+    uint32_t v = 0;
+    for (uint32_t k = 0; k < 4; ++k)
+        if (i + k < end) v |= (uint32_t)p[i + k] << (8 * k);
+    return v;
+}
+// 16 bytes of p[i, i+16), bytes at or past `end` read as 0.  (Loading the
+// one or two aligned 16-B blocks that hold a partial window and shifting
+// them into place was slower for framing and deframing alike, round 3:
+// profiles/r03w_tail_ab/.)
 __device__ __forceinline__ u32x4 ld16_upto(const uint8_t *p, uint64_t i, uint64_t end) {
     if (i + 16 <= end) return ld16(p + i);
     u32x4 v = {ld4_upto(p, i, end), ld4_upto(p, i + 4, end), ld4_upto(p, i + 8, end), ld4_upto(p, i + 12, end)};
@@ -292,9 +295,79 @@ __global__ __launch_bounds__(256) void k_flag_count(const uint8_t *buf, uint64_t
     if (threadIdx.x == 0) cnt[blockIdx.x] = s;
 }
 
+// wave-wide inclusive prefix sum: row scans, then the lower rows' totals
+// (readlane) added in
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x = row_incl_scan16(x);
+    const uint32_t r0 = __builtin_amdgcn_readlane(x, 15), r1 = __builtin_amdgcn_readlane(x, 31),
+                   r2 = __builtin_amdgcn_readlane(x, 47);
+    const uint32_t lane = threadIdx.x & 63u;
+    return x + (lane >= 16u ? r0 : 0u) + (lane >= 32u ? r1 : 0u) + (lane >= 48u ? r2 : 0u);
+}
+
+#ifndef RNSTOK_FLAG_SCATTER_SPANS
+// Flag positions in stream order.  cnt_off + part: the chunk counts' scan
+// within blocks of SCAN_BLOCK chunks and the blocks' scanned totals (the
+// scan's third launch, adding the two, is folded in here).  Thread t loads the 16-B units t, t+256,
+// t+512, t+768 of its chunk (each load instruction 1 KiB contiguous across a
+// wave, as k_flag_count); the stream-order rank of a unit's flags is the
+// block's flags in the earlier 4 KiB quarters plus those of the lower threads
+// in its own quarter: the four per-thread counts (<= 16 each, <= 4096 per
+// block) ride as 16-bit fields of two words through one wave scan each and
+// one LDS exchange of the wave totals.  The form with 64 contiguous bytes
+// per thread (RNSTOK_FLAG_SCATTER_SPANS) loaded at a 64-B lane stride and
+// ranked with an 8-step LDS scan (16 barriers).
+__global__ __launch_bounds__(256) void k_flag_scatter(const uint8_t *buf, uint64_t len, const uint64_t *cnt_off,
+                                                      const uint64_t *part, uint64_t *pos) {
+    const uint64_t cbase = (uint64_t)blockIdx.x * FLAG_CHUNK;
+    const uint32_t t = threadIdx.x, wave = t >> 6;
+    uint32_t m[4][4], c[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint64_t u = cbase + 4096ull * k + 16ull * t;
+        const u32x4 v = u < len ? ld16_upto(buf, u, len) : u32x4{0u, 0u, 0u, 0u};
+        m[k][0] = eqbytes(v.x, 0x7E7E7E7Eu); m[k][1] = eqbytes(v.y, 0x7E7E7E7Eu);
+        m[k][2] = eqbytes(v.z, 0x7E7E7E7Eu); m[k][3] = eqbytes(v.w, 0x7E7E7E7Eu);
+        c[k] = __builtin_popcount(m[k][0]) + __builtin_popcount(m[k][1]) + __builtin_popcount(m[k][2]) +
+               __builtin_popcount(m[k][3]);
+    }
+    const uint32_t lo = c[0] | c[1] << 16, hi = c[2] | c[3] << 16;
+    const uint32_t ilo = wave_incl_scan(lo), ihi = wave_incl_scan(hi);
+    __shared__ uint32_t wtot[2][4];
+    if ((t & 63u) == 63u) {
+        wtot[0][wave] = ilo;
+        wtot[1][wave] = ihi;
+    }
+    __syncthreads();
+    uint32_t plo = 0, phi = 0, tlo = 0, thi = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 4; ++w) {
+        const uint32_t a = wtot[0][w], b = wtot[1][w];
+        plo += w < wave ? a : 0u;
+        phi += w < wave ? b : 0u;
+        tlo += a;
+        thi += b;
+    }
+    const uint32_t elo = plo + ilo - lo, ehi = phi + ihi - hi;
+    const uint32_t excl[4] = {elo & 0xFFFFu, elo >> 16, ehi & 0xFFFFu, ehi >> 16};
+    const uint32_t tot[4] = {tlo & 0xFFFFu, tlo >> 16, thi & 0xFFFFu, thi >> 16};
+    const uint64_t base = cnt_off[blockIdx.x] + part[blockIdx.x / SCAN_BLOCK];
+    uint32_t before = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        if (c[k]) {
+            uint64_t w = base + before + excl[k];
+            const uint64_t u = cbase + 4096ull * k + 16ull * t;
+            for (uint32_t j = 0; j < 4; ++j)
+                for (uint32_t f = m[k][j]; f; f &= f - 1) pos[w++] = u + 4 * j + (__builtin_ctz(f) >> 3);
+        }
+        before += tot[k];
+    }
+}
+#else
 // flag positions in stream order: thread t owns bytes [64t, 64t+64) of its chunk
 __global__ __launch_bounds__(256) void k_flag_scatter(const uint8_t *buf, uint64_t len, const uint64_t *cnt_off,
-                                                      uint64_t *pos) {
+                                                      const uint64_t *part, uint64_t *pos) {
     const uint64_t base = (uint64_t)blockIdx.x * FLAG_CHUNK + threadIdx.x * 64ull;
     uint32_t m[16], c = 0;
 #pragma unroll
@@ -316,10 +389,11 @@ __global__ __launch_bounds__(256) void k_flag_scatter(const uint8_t *buf, uint64
         __syncthreads();
     }
     if (c == 0) return;
-    uint64_t w = cnt_off[blockIdx.x] + sh[threadIdx.x] - c;
+    uint64_t w = cnt_off[blockIdx.x] + part[blockIdx.x / SCAN_BLOCK] + sh[threadIdx.x] - c;
     for (uint32_t k = 0; k < 16; ++k)
         for (uint32_t f = m[k]; f; f &= f - 1) pos[w++] = base + 4 * k + (__builtin_ctz(f) >> 3);
 }
+#endif
 
 // One DPP row (16 lanes x 16 B) per consecutive flag pair (k, k+1), 4 pairs
 // per wave: the read loop's frame buf[pos_k+1 : pos_{k+1}) with its two
@@ -332,11 +406,15 @@ __global__ __launch_bounds__(256) void k_flag_scatter(const uint8_t *buf, uint64
 // words shifted by one byte); the byte before a frame is its opening flag and
 // the byte after it the closing flag, so neither rule fires across the frame
 // edge.  Kept bytes are placed with a row prefix sum.
-__global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, const uint64_t *pos, const uint64_t *nflags_p,
-                                                       uint64_t max_pairs, uint32_t hw_mtu, uint32_t ifac_size,
-                                                       uint8_t *out, uint64_t *frame_off, uint32_t *frame_len,
-                                                       int32_t *status) {
+__device__ void deframe_counts(const uint64_t *nflags_p, const uint64_t *pos, uint64_t len, uint32_t hw_mtu,
+                               uint64_t *counts);
+__global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, uint64_t len, const uint64_t *pos,
+                                                       const uint64_t *nflags_p, uint64_t max_pairs, uint32_t hw_mtu,
+                                                       uint32_t ifac_size, uint8_t *out, uint64_t *frame_off,
+                                                       uint32_t *frame_len, int32_t *status, uint64_t *counts) {
     __shared__ SelTables tab;
+    // the pair count and the bytes consumed (k_deframe_counts' job, folded in: one launch fewer)
+    if (blockIdx.x == 0 && threadIdx.x == 0) deframe_counts(nflags_p, pos, len, hw_mtu, counts);
     fill_sel_tables(&tab);
     const uint64_t nf = *nflags_p;
     uint64_t npairs = nf > 1 ? nf - 1 : 0;
@@ -359,7 +437,29 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, const
         for (uint64_t w = a; w < e; w += 256u) {
             const uint64_t b = w + 16u * rl;
             const uint32_t nb = b < e ? (uint32_t)min((uint64_t)16, e - b) : 0u;
+#ifndef RNSTOK_UNESC_BYTE_TAIL
+            // a window's last lane: one 16-B load with the bytes past the
+            // frame masked off, unless the load would run past the stream
+            // (the byte-wise form issues up to 15 loads one after another)
+            u32x4 v = u32x4{0u, 0u, 0u, 0u};
+            if (nb == 16u || (nb && b + 16u <= len)) {
+                v = ld16(buf + b);
+                if (nb < 16u) {
+                    uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
+                    if (nb <= 8u) {
+                        hi = 0;
+                        lo = nb == 8u ? lo : lo & ((1ull << (8u * nb)) - 1ull);
+                    } else {
+                        hi &= (1ull << (8u * (nb - 8u))) - 1ull;
+                    }
+                    v = u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+                }
+            } else if (nb) {
+                v = ld16_upto(buf, b, e);
+            }
+#else
             const u32x4 v = nb ? ld16_upto(buf, b, e) : u32x4{0u, 0u, 0u, 0u};
+#endif
             uint32_t prevb = dpp<0x111>(v.w) >> 24;          // row_shr:1: the previous lane's last byte
             if (rl == 0) prevb = carry;
             uint32_t nextb = dpp<0x101>(v.x) & 0xFFu;         // row_shl:1: the next lane's first byte
@@ -404,6 +504,68 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, const
             const uint32_t kept = nb - ndrop;
             const uint32_t incl = row_incl_scan16(kept);
             uint8_t *q = o + kept_total + (incl - kept);
+#ifndef RNSTOK_UNESC_WORD_STORES
+            // Row-wide 16-B stores.  The lane's kept bytes are packed low in
+            // c[0..3] (each word through its compaction selector, the pieces
+            // placed with 64-bit shifts).  A lane then stores 16 bytes at its
+            // output position: its own kept bytes followed by the next lane's
+            // first 16 - kept, which that lane stores too, with the same
+            // values, so the overlap is benign; nothing past the row's output
+            // is written.  Lanes that cannot borrow enough from their
+            // neighbour (the row's last lane, the frame's last lane, lanes
+            // with fewer than 8 kept bytes) store exactly their bytes.  The
+            // per-word form (RNSTOK_UNESC_WORD_STORES) stored every word of an
+            // escape-holding lane as a dword plus single bytes.
+            uint32_t c[4] = {y[0], y[1], y[2], y[3]};
+            if (kept != 16u) {
+                uint64_t lo = 0, hi = 0;
+                uint32_t at = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint32_t m = nb > 4u * j ? min(4u, nb - 4u * j) : 0u;
+                    const uint32_t keep = byte_pattern(~drop[j] & 0x80808080u) & ((1u << m) - 1u);
+                    const uint64_t piece = __builtin_amdgcn_perm(y[j], 0u, tab.compact[keep]);
+                    if (at < 8u) {
+                        lo |= piece << (8u * at);
+                        if (at > 4u) hi |= piece >> (8u * (8u - at));
+                    } else {
+                        hi |= piece << (8u * (at - 8u));
+                    }
+                    at += __builtin_popcount(keep);
+                }
+                c[0] = (uint32_t)lo; c[1] = (uint32_t)(lo >> 32); c[2] = (uint32_t)hi; c[3] = (uint32_t)(hi >> 32);
+            }
+            // the next lane's first 8 kept bytes and its count (row_shl:1; the row's last lane reads 0)
+            const uint32_t n0 = dpp<0x101>(c[0]), n1 = dpp<0x101>(c[1]), kn = dpp<0x101>(kept);
+            const uint64_t up = ((uint64_t)c[3] << 32) | c[2];
+            if (rl != 15u && kept >= 8u && kept + kn >= 16u) {
+                const uint32_t t = kept - 8u;       // own bytes in the upper half: 0..8
+                const uint64_t nx = ((uint64_t)n1 << 32) | n0;
+                const uint64_t w = t == 8u ? up : ((up & ((1ull << (8u * t)) - 1ull)) | (nx << (8u * t)));
+                st16(q, u32x4{c[0], c[1], (uint32_t)w, (uint32_t)(w >> 32)});
+            } else if (kept == 16u) {
+                st16(q, u32x4{c[0], c[1], c[2], c[3]});
+            } else if (kept) {
+                uint64_t v64 = ((uint64_t)c[1] << 32) | c[0];
+                uint32_t k = kept;
+                uint8_t *d = q;
+                if (k >= 8u) {
+                    __builtin_memcpy(d, &v64, 8);
+                    d += 8; k -= 8u; v64 = up;
+                }
+                if (k >= 4u) {
+                    const uint32_t w4 = (uint32_t)v64;
+                    __builtin_memcpy(d, &w4, 4);
+                    d += 4; k -= 4u; v64 >>= 32;
+                }
+                if (k >= 2u) {
+                    const uint16_t w2 = (uint16_t)v64;
+                    __builtin_memcpy(d, &w2, 2);
+                    d += 2; k -= 2u; v64 >>= 16;
+                }
+                if (k) *d = (uint8_t)v64;
+            }
+#else
             if (ndrop == 0 && nb == 16) {
                 st16(q, u32x4{y[0], y[1], y[2], y[3]});
             } else if (nb) {
@@ -420,6 +582,7 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, const
                     }
                 }
             }
+#endif
             kept_total += row_sum16(kept);
             carry = row_sum16(rl == 15 ? v.w >> 24 : 0u);      // the window's last byte, to every lane
         }
@@ -436,8 +599,8 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, const
     }
 }
 
-__global__ void k_deframe_counts(const uint64_t *nflags_p, const uint64_t *pos, uint64_t len, uint32_t hw_mtu,
-                                 uint64_t *counts) {
+__device__ __forceinline__ void deframe_counts(const uint64_t *nflags_p, const uint64_t *pos, uint64_t len,
+                                               uint32_t hw_mtu, uint64_t *counts) {
     const uint64_t nf = *nflags_p;
     counts[0] = nf > 1 ? nf - 1 : 0;
     // What the loop keeps for the next read (TCPInterface.py:391-411): after a
@@ -454,6 +617,10 @@ __global__ void k_deframe_counts(const uint64_t *nflags_p, const uint64_t *pos, 
         consumed = (len - last > 2ull * hw_mtu) ? len : last;
     }
     counts[1] = consumed;
+}
+__global__ void k_deframe_counts(const uint64_t *nflags_p, const uint64_t *pos, uint64_t len, uint32_t hw_mtu,
+                                 uint64_t *counts) {
+    deframe_counts(nflags_p, pos, len, hw_mtu, counts);
 }
 
 // ------------------------------------------------------------------ IFAC --
@@ -750,21 +917,27 @@ hipError_t launch_hdlc_deframe(const uint8_t *buf, uint64_t len, uint32_t hw_mtu
     uint64_t *cnt = (uint64_t *)ws;
     uint64_t *cnt_off = cnt + chunks;
     uint64_t *part = cnt_off + chunks;
-    uint64_t *nflags = part + (chunks + SCAN_BLOCK - 1) / SCAN_BLOCK + 1;
-    uint64_t *pos = nflags + 1;
-    hipError_t e = hipMemsetAsync(nflags, 0, 8, s);
-    if (e != hipSuccess) return e;
+    // part[nb] receives the scanned total (k_scan_parts): the flag count
+    uint64_t *nflags = part + (chunks + SCAN_BLOCK - 1) / SCAN_BLOCK;
+    uint64_t *pos = nflags + 2;
+    hipError_t e;
+    if (!chunks && (e = hipMemsetAsync(nflags, 0, 8, s)) != hipSuccess) return e;   // else k_scan_parts writes it
     if (chunks) {
         hipLaunchKernelGGL(k_flag_count, dim3((unsigned)chunks), dim3(256), 0, s, buf, len, cnt);
-        if ((e = launch_scan(cnt, cnt_off, chunks, part, nflags, s)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_flag_scatter, dim3((unsigned)chunks), dim3(256), 0, s, buf, len, cnt_off, pos);
+        // chunk counts scanned within blocks, then the block totals (part[nb] = the flag count);
+        // the scatter adds the two
+        const uint64_t nb = (chunks + SCAN_BLOCK - 1) / SCAN_BLOCK;
+        hipLaunchKernelGGL(k_scan_block, dim3((unsigned)nb), dim3(SCAN_BLOCK), 0, s, cnt, cnt_off, part, chunks);
+        hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(SCAN_BLOCK), 0, s, part, nb);
+        hipLaunchKernelGGL(k_flag_scatter, dim3((unsigned)chunks), dim3(256), 0, s, buf, len, cnt_off, part, pos);
     }
-    hipLaunchKernelGGL(k_deframe_counts, dim3(1), dim3(1), 0, s, nflags, pos, len, hw_mtu, counts);
     // the pair count lives on the device: a grid-stride kernel sized by the caller's capacity
     if (max_pairs) {
         const uint64_t g = min((max_pairs + 15) / 16, (uint64_t)WAVE_GRID);   // one DPP row per frame
-        hipLaunchKernelGGL(k_hdlc_unescape, dim3((unsigned)g), dim3(256), 0, s, buf, pos, nflags, max_pairs, hw_mtu,
-                           ifac_size, out, frame_off, frame_len, status);
+        hipLaunchKernelGGL(k_hdlc_unescape, dim3((unsigned)g), dim3(256), 0, s, buf, len, pos, nflags, max_pairs,
+                           hw_mtu, ifac_size, out, frame_off, frame_len, status, counts);
+    } else {
+        hipLaunchKernelGGL(k_deframe_counts, dim3(1), dim3(1), 0, s, nflags, pos, len, hw_mtu, counts);
     }
     return hipGetLastError();
 }

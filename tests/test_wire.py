@@ -274,3 +274,42 @@ def test_gpu_device_forms_match_host_forms():
         assert bool(f[i]["ok"]) == (ref[i] is not None)
         if ref[i]:
             assert bytes(f[i]["packet_hash"]) == ref[i]["packet_hash"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("density", [0.0, 0.02, 0.3, 0.9])
+def test_gpu_deframe_escape_dense_writes_only_frames(density):
+    """Unescape's row-wide 16-B stores (a lane stores its kept bytes and then
+    its neighbour's first ones, which the neighbour stores too): frames of
+    0-700 B whose bytes are 7E/7D with the given probability (lanes with many
+    escapes keep as few as 8 of their 16 bytes) come back exact, and no byte of
+    the output buffer outside the frames' own output is written."""
+    import torch
+    from reticulum_amd import device, wire
+    rng = np.random.Generator(np.random.PCG64(int(density * 1000) + 7))
+    pk = []
+    for n in rng.integers(0, 700, 3000):
+        a = rng.integers(0, 256, int(n), dtype=np.uint8)
+        hit = rng.random(int(n)) < density
+        a[hit] = rng.choice(np.array([0x7E, 0x7D], np.uint8), int(hit.sum()))
+        pk.append(a.tobytes())
+    stream, _ = wire.hdlc_frame_batch(pk)
+    dev = torch.device("cuda", 0)
+    buf = torch.from_numpy(np.frombuffer(stream, np.uint8).copy()).to(dev)
+    total = len(stream)
+    pairs = 2 * len(pk)
+    out = torch.full((total,), 0xA5, dtype=torch.uint8, device=dev)
+    d_off = torch.empty(pairs, dtype=torch.int64, device=dev)
+    d_len = torch.empty(pairs, dtype=torch.int32, device=dev)
+    d_st = torch.empty(pairs, dtype=torch.int32, device=dev)
+    cnt = torch.empty(2, dtype=torch.int64, device=dev)
+    device.hdlc_deframe(buf, out, d_off, d_len, d_st, cnt)
+    o = out.cpu().numpy()
+    k = int(cnt[0])
+    do, dl, ds = d_off.cpu().numpy()[:k], d_len.cpu().numpy()[:k], d_st.cpu().numpy()[:k]
+    frames = [o[int(do[i]):int(do[i]) + int(dl[i])].tobytes() for i in range(k) if ds[i] == wire.FRAME_OK]
+    assert frames == [p for p in pk if len(p) > 19]
+    written = np.zeros(total, bool)
+    for i in range(k):
+        written[int(do[i]):int(do[i]) + int(dl[i])] = True
+    assert (o[~written] == 0xA5).all()

@@ -180,6 +180,7 @@ __device__ __forceinline__ void fill_sel_tables(SelTables *t) {
 __device__ __forceinline__ uint32_t byte_pattern(uint32_t m) {
     return ((((m >> 7) & 0x01010101u) * 0x01020408u) >> 24) & 0xFu;
 }
+#if defined(RNSTOK_FRAME_WORD_STORES) || defined(RNSTOK_UNESC_WORD_STORES)
 __device__ __forceinline__ void st4u(uint8_t *p, uint32_t v) { __builtin_memcpy(p, &v, 4); }
 // exactly n (0..8) bytes of lo||hi at q: whole dwords where they fit, bytes for the rest
 __device__ __forceinline__ void st_exact8(uint8_t *q, uint32_t lo, uint32_t hi, uint32_t n) {
@@ -194,6 +195,43 @@ __device__ __forceinline__ void st_exact8(uint8_t *q, uint32_t lo, uint32_t hi, 
         return;
     }
     for (uint32_t t = 0; t < n; ++t) q[t] = (uint8_t)(lo >> (8 * t));
+}
+#endif
+
+// exactly k (0..16) bytes of lo||hi at d: a 16-B store, or 8/4/2/1-byte pieces
+__device__ __forceinline__ void st_exact16(uint8_t *d, uint64_t lo, uint64_t hi, uint32_t k) {
+    if (k == 16u) {
+        st16(d, u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)});
+        return;
+    }
+    if (k >= 8u) {
+        __builtin_memcpy(d, &lo, 8);
+        d += 8; k -= 8u; lo = hi;
+    }
+    if (k >= 4u) {
+        const uint32_t w = (uint32_t)lo;
+        __builtin_memcpy(d, &w, 4);
+        d += 4; k -= 4u; lo >>= 32;
+    }
+    if (k >= 2u) {
+        const uint16_t w = (uint16_t)lo;
+        __builtin_memcpy(d, &w, 2);
+        d += 2; k -= 2u; lo >>= 16;
+    }
+    if (k) *d = (uint8_t)lo;
+}
+// own (the first t < 16 bytes of lo||hi, the rest 0) followed by the first
+// 16 - t bytes of nlo||nhi
+__device__ __forceinline__ void funnel16(uint64_t &lo, uint64_t &hi, uint64_t nlo, uint64_t nhi, uint32_t t) {
+    if (t < 8u) {
+        const uint32_t r = 8u * t;
+        hi = t ? (nlo >> (64u - r)) | (nhi << r) : nhi;
+        lo |= t ? nlo << r : nlo;
+    } else if (t == 8u) {
+        hi = nlo;
+    } else {
+        hi |= nlo << (8u * (t - 8u));
+    }
 }
 
 __global__ __launch_bounds__(256) void k_hdlc_count(const uint8_t *pkt, const uint64_t *off, const uint32_t *len,
@@ -239,6 +277,53 @@ __global__ __launch_bounds__(256) void k_hdlc_write(const uint8_t *pkt, const ui
             const uint32_t sz = nb + esc;
             const uint32_t incl = row_incl_scan16(sz);
             uint8_t *q = o + base + (incl - sz);
+#ifndef RNSTOK_FRAME_WORD_STORES
+            // HDLC.escape (TCPInterface.py:50-52: ESC first, then FLAG; per
+            // byte the same: 7D x^0x20): each word expands through one
+            // selector pair into 4..8 bytes; the lane's sz expanded bytes are
+            // packed in a[0..3] with 64-bit shifts.  Stores are row-wide as in
+            // unescape: 16 B at q, and the rest (sz - 16 bytes) completed with
+            // the next lane's first output bytes, which that lane stores too
+            // with the same values; the row's last lane and a packet's last
+            // lane store exactly.  (RNSTOK_FRAME_WORD_STORES: every word of an
+            // escaping lane stored as a dword plus single bytes.)
+            uint64_t a[4] = {((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z, 0ull, 0ull};
+            if (esc) {
+                const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+                a[0] = a[1] = 0ull;
+                uint32_t at = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint32_t e = escbytes(wv[j]);                // bytes past nb are 0: never escape
+                    const uint32_t pat = byte_pattern(e);
+                    const uint32_t x = wv[j] ^ (e >> 2);               // 0x80 -> 0x20 in the escaped bytes
+                    const uint64_t piece = ((uint64_t)__builtin_amdgcn_perm(x, 0x7D7D7D7Du, tab.expand[pat][1]) << 32) |
+                                           __builtin_amdgcn_perm(x, 0x7D7D7D7Du, tab.expand[pat][0]);
+                    const uint32_t k = at >> 3, r = 8u * (at & 7u);
+                    const uint64_t pl = piece << r, ph = r ? piece >> (64u - r) : 0ull;
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) a[i] |= (i == k ? pl : 0ull) | (i == k + 1u ? ph : 0ull);
+                    at += 4u * j < nb ? min(4u, nb - 4u * j) + __builtin_popcount(e) : 0u;
+                }
+            }
+            // the next lane's first 16 output bytes and its size (row_shl:1; the row's last lane reads 0)
+            const uint64_t n0 = ((uint64_t)dpp<0x101>((uint32_t)(a[0] >> 32)) << 32) | dpp<0x101>((uint32_t)a[0]);
+            const uint64_t n1 = ((uint64_t)dpp<0x101>((uint32_t)(a[1] >> 32)) << 32) | dpp<0x101>((uint32_t)a[1]);
+            const uint32_t szn = dpp<0x101>(sz);
+            if (sz >= 16u) {
+                st16(q, u32x4{(uint32_t)a[0], (uint32_t)(a[0] >> 32), (uint32_t)a[1], (uint32_t)(a[1] >> 32)});
+                const uint32_t t = sz - 16u;
+                if (t == 16u || (t && rl != 15u && szn >= 16u - t)) {
+                    uint64_t lo = a[2], hi = a[3];
+                    if (t < 16u) funnel16(lo, hi, n0, n1, t);
+                    st16(q + 16, u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)});
+                } else if (t) {
+                    st_exact16(q + 16, a[2], a[3], t);
+                }
+            } else if (sz) {
+                st_exact16(q, a[0], a[1], sz);
+            }
+#else
             if (esc == 0 && nb == 16) {
                 st16(q, v);
             } else if (nb) {
@@ -260,6 +345,7 @@ __global__ __launch_bounds__(256) void k_hdlc_write(const uint8_t *pkt, const ui
                     }
                 }
             }
+#endif
             base += row_sum16(sz);
         }
         if (rl == 0 && valid) o[base] = FLAG;

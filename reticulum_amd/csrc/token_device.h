@@ -97,17 +97,12 @@ struct Lanes {
 // v_bitop3; bytes 0, 2, 3 take one (half-rate) v_perm_b32.
 template <int K, int REGION>
 __device__ __forceinline__ uint32_t taddr(uint32_t s, const Lanes &L) {
-#ifndef RNSTOK_SHIFT_ADDR
+    // (Bytes 0, 2, 3 by a shift to bits 8..15 plus the same and_or, two
+    // dual-issuable ops instead of one v_perm, was 7-11 % slower on c2/c3 and
+    // 14 % on the c4 shard: the kernels' mixed streams do not pair them,
+    // profiles/r03e_shift_addr_ab.txt.)
     if (K == 1) return and_or(s, L.m8, REGION ? L.r1 : L.r0);
     return perm(s, L.r1, REGION ? Sel<K>::R1 : Sel<K>::R0);
-#else
-    // Experiment (round 3, not the product): bytes 0, 2, 3 by a shift to bits
-    // 8..15 and the same and_or, two dual-issuable ops instead of one v_perm
-    // (which always takes a 4-cycle issue slot alone).  7-11 % slower on c2/c3
-    // and 14 % on the c4 shard (profiles/r03e_shift_addr_ab.txt).
-    const uint32_t t = K == 0 ? (s << 8) : (K == 1 ? s : (s >> (8 * K - 8)));
-    return and_or(t, L.m8, REGION ? L.r1 : L.r0);
-#endif
 }
 
 // One T-table round column: T0[a.b0] ^ T1[b.b1] ^ T2[c.b2] ^ T3[d.b3] ^ k
@@ -138,15 +133,6 @@ __device__ __forceinline__ void tround_mix(uint32_t s[4], const uint32_t v[16], 
     for (int j = 0; j < 4; ++j) s[j] = xor3(xor3(v[4 * j], v[4 * j + 1], v[4 * j + 2]), v[4 * j + 3], k[j]);
 }
 
-// Optional scheduling fence around the SHA round inside each AES round
-// (the compiler may not move instructions across it).  Off by default: left
-// to the scheduler, c2 decrypt is 0.9 % and c3 encrypt/decrypt 1.8 / 2.4 %
-// faster, c2 encrypt unchanged (30-round A/B with duplicate builds).
-#ifdef RNSTOK_SCHED_FENCE
-#define RT_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define RT_FENCE() ((void)0)
-#endif
 
 // Encryption final round column: row r from the table whose byte r is S[x]
 // (row0 <- T2, row1 <- T3, row2 <- T0, row3 <- T1), merged by byte masks.
@@ -368,11 +354,9 @@ __device__ __forceinline__ void enc_quad(u32x4 c[4], const u32x4 x[4], u32x4 cha
         for (int r = 1; r < NR; ++r) {
             uint32_t v[16];
             tround_load<false>(v, st, L);      // 16 LDS lookups in flight ...
-            if (WITH_SHA) {
-                RT_FENCE();
-                S.round(b * NR + r - 1);        // ... while one SHA-256 round issues
-                RT_FENCE();
-            }
+            // ... while one SHA-256 round issues (a sched_barrier on either
+            // side of it was 0.9-2.4 % slower on c2 decrypt and c3)
+            if (WITH_SHA) S.round(b * NR + r - 1);
             tround_mix(st, v, rk + 4 * r);
         }
         const uint32_t s0 = st[0], s1 = st[1], s2 = st[2], s3 = st[3];
@@ -406,11 +390,7 @@ __device__ __forceinline__ void dec_quad(u32x4 p[4], const u32x4 c[4], u32x4 cha
         for (int b = 0; b < 4; ++b) {
             uint32_t v[16];
             tround_load<true>(v, s[b], L);
-            if (WITH_SHA) {
-                RT_FENCE();
-                S.round((r - 1) * 4 + b);
-                RT_FENCE();
-            }
+            if (WITH_SHA) S.round((r - 1) * 4 + b);
             tround_mix(s[b], v, dk + 4 * r);
         }
     }

@@ -464,41 +464,25 @@ __global__ __launch_bounds__(256) void k_encrypt_long(EncArgs a) {
 // one barrier per quad step.  Single key, uniform lengths.
 // Hashing waves: 4 (one per SIMD, 32 tokens each) measured 8 % slower than 2
 // on the c4 shard (profiles/r03g_long4_ab.txt).
-#ifndef RNSTOK_L4_HASH_WAVES
-#define RNSTOK_L4_HASH_WAVES 2
-#endif
-constexpr uint32_t L4_TOK = 128, L4_AES_WAVES = 8, L4_HASH_WAVES = RNSTOK_L4_HASH_WAVES;
+constexpr uint32_t L4_TOK = 128, L4_AES_WAVES = 8, L4_HASH_WAVES = 2;
 constexpr uint32_t L4_THREADS = 64u * (L4_AES_WAVES + L4_HASH_WAVES), L4_HASH_TOK = L4_TOK / L4_HASH_WAVES;
 static_assert(L4_HASH_TOK <= 64u && L4_TOK % L4_HASH_WAVES == 0u, "one token per hashing lane");
 
-// Ring layout: token t's quad (4 blocks x 16 B) at t*64 B, block i in 16-B
-// unit i ^ l4_swz(t).  Unswizzled, the AES lanes' 4-B stores (lanes of 8
-// consecutive tokens x 4 columns) meet 4-way and the hashing lanes' 16-B
-// reads (one token per lane) 4-way bank conflicts (7 % of the kernel's LDS
-// cycles, profiles/r02e_c4s8_pmc_summary.txt).  RNSTOK_L4_SWIZZLE makes both
-// conflict-free for ds_write_b32's 2 x 32 and ds_read_b128's 4 x 16 lane
-// groups (MI355X_MICROARCH.md LDS table; exhaustive check in DESIGN.md §4.2),
-// but measured 1.2 % slower on the c4 shard (1.001 vs 0.989 ms,
+// Ring layout: token t's quad (4 blocks x 16 B) at t*64 B.  The AES lanes'
+// 4-B stores (lanes of 8 consecutive tokens x 4 columns) meet 4-way and the
+// hashing lanes' 16-B reads (one token per lane) 4-way bank conflicts (7 % of
+// the kernel's LDS cycles, profiles/r02e_c4s8_pmc_summary.txt).  A swizzle
+// that makes both conflict-free (block i in 16-B unit i ^ (((t >> 1) ^ (t >>
+// 2)) & 3)) measured 1.2 % slower on the c4 shard (1.001 vs 0.989 ms,
 // profiles/r03g_long4_ab.txt): the LDS pipe is not what bounds this kernel.
-__device__ __forceinline__ uint32_t l4_swz(uint32_t t) {
-#ifdef RNSTOK_L4_SWIZZLE
-    return ((t >> 1) ^ (t >> 2)) & 3u;
-#else
-    return 0u * t;
-#endif
-}
 constexpr uint32_t L4_RING = LDS_ENC_BYTES;                              // after the table image
-// The ring holds 2 * L4_PHASE quads: AES waves fill L4_PHASE quads per
-// barrier while the hashing waves consume the previous L4_PHASE.  Two quads
-// per phase (half the barriers, a 160 KiB image) measured the same as one
-// (c4 shard 0.999 vs 0.997 ms): the fused kernel's excess over its AES side
-// alone (0.91 ms; hashing side alone 0.73) is SIMD contention, not barrier
-// jitter.
-#ifndef RNSTOK_L4_PHASE
-#define RNSTOK_L4_PHASE 1
-#endif
-constexpr uint32_t L4_PHASE = RNSTOK_L4_PHASE, L4_SLOTS = 2u * L4_PHASE;
-constexpr uint32_t LDS_ENC_LONG4_BYTES = L4_RING + L4_SLOTS * L4_TOK * 64u;   // + slots x 128 tokens x 64 B
+// The ring holds 2 quads per token: AES waves fill one per barrier while the
+// hashing waves consume the other.  Two quads per phase (half the barriers, a
+// 160 KiB image) measured the same as one (c4 shard 0.999 vs 0.997 ms): the
+// fused kernel's excess over its AES side alone (0.91 ms; hashing side alone
+// 0.73) is SIMD contention, not barrier jitter.
+constexpr uint32_t L4_SLOTS = 2u;
+constexpr uint32_t LDS_ENC_LONG4_BYTES = L4_RING + L4_SLOTS * L4_TOK * 64u;   // + 2 slots x 128 tokens x 64 B
 
 // DPP quad_perm: lane j of each group of four reads lane (j + K) & 3.
 template <int K>
@@ -538,19 +522,12 @@ __device__ __forceinline__ uint32_t enc_block4(uint32_t s, const uint32_t *rk, c
         // bound, and this is a shorter dependent path than the three
         // v_xor_b32_dpp in a row the compiler folds the plain XORs into
         // (c4 shard encrypt 1.044 -> 0.992 ms, A/B)
-#ifdef RNSTOK_L4_FOLD
-        // experiment (round 3): two of the moves carry an XOR (v_xor_b32 with
-        // a DPP source: the round key and this lane's own term ride on them),
-        // one xor3 after the moves instead of two in a row.  3.8 % slower on
-        // the c4 shard (1.026 vs 0.989 ms, profiles/r03g_long4_ab.txt).
-        uint32_t x1 = quad_rot<1>(u1) ^ u0, x2 = quad_rot<2>(u2) ^ rk[r], x3 = quad_rot<3>(u3);
-        asm volatile("" : "+v"(x1), "+v"(x2), "+v"(x3));
-        s = xor3(x1, x2, x3);
-#else
+        // (Two of the moves carrying an XOR, v_xor_b32 with a DPP source,
+        // and one xor3 after them: 12 instructions per round instead of 13
+        // but 3.8 % slower on the c4 shard, profiles/r03g_long4_ab.txt.)
         uint32_t x1 = quad_rot<1>(u1), x2 = quad_rot<2>(u2), x3 = quad_rot<3>(u3);
         asm volatile("" : "+v"(x1), "+v"(x2), "+v"(x3));
         s = xor3(xor3(x1, x2, x3), u0, rk[r]);
-#endif
     }
     // final round: byte k of column j is S[s_{j+k}.b_k] (tlast_enc, split the same way)
     const uint32_t v0 = lds(taddr<0, 1>(s, L), 0) & 0x000000ffu, v1 = lds(taddr<1, 1>(s, L), 128) & 0x0000ff00u;
@@ -572,7 +549,6 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
     const uint32_t col = threadIdx.x & 3u;
     const bool hash_lane = aes || lane < L4_HASH_TOK;
     const uint32_t slot = aes ? threadIdx.x >> 2 : (wave - L4_AES_WAVES) * L4_HASH_TOK + (hash_lane ? lane : 0u);
-    const uint32_t swz = l4_swz(slot);
     const uint32_t L = a.uni_len, nfull = L >> 4, nq = nfull >> 2, tb = (nfull & 3u) + 1u, rem = L & 15u;
     uint32_t rk[NR + 1];
 #pragma unroll
@@ -618,10 +594,10 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
                     if (valid && (uint32_t)b < nst) st32u(Ck + 16 * b, cq[b]);
                 lds_w *ring = (lds_w *)(uintptr_t)(L4_RING + ((k % L4_SLOTS) * L4_TOK + slot) * 64u + 4u * col);
 #pragma unroll
-                for (int b = 0; b < 4; ++b) ring[4u * ((uint32_t)b ^ swz)] = cq[b];
-                // end of a phase: its quads become visible to the hashing
-                // waves, which are done with the previous phase's slots
-                if ((k + 1u) % L4_PHASE == 0u || k == nq) __syncthreads();
+                for (int b = 0; b < 4; ++b) ring[4u * (uint32_t)b] = cq[b];
+                // the quad becomes visible to the hashing waves, which are
+                // done with the previous one's slot
+                __syncthreads();
             }
             __syncthreads();         // matches the hashing waves' last phase
         } else {
@@ -630,12 +606,10 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
             load_uniform8(opad, a.rec + REC_OPAD);
             u32x4 prev = valid ? ld16(a.iv + 16ull * p) : u32x4{0u, 0u, 0u, 0u};
             const uint64_t bits = (uint64_t)(64u + 16u + 16u * (nfull + 1u)) * 8u;
-            __syncthreads();         // phase 0: nothing to hash yet
-            const uint32_t phases = (nq + L4_PHASE) / L4_PHASE;       // the AES waves' phases
-            for (uint32_t j = 1; j <= phases; ++j) {
-              for (uint32_t q = (j - 1u) * L4_PHASE; q < j * L4_PHASE && q <= nq; ++q) {
+            __syncthreads();         // step 0: nothing to hash yet
+            for (uint32_t q = 0; q <= nq; ++q) {
                 lds_q *r = (lds_q *)(uintptr_t)(L4_RING + ((q % L4_SLOTS) * L4_TOK + slot) * 64u);
-                const u32x4 c0 = r[0u ^ swz], c1 = r[1u ^ swz], c2 = r[2u ^ swz], c3 = r[3u ^ swz];
+                const u32x4 c0 = r[0], c1 = r[1], c2 = r[2], c3 = r[3];
                 if (q < nq) {
 #ifndef RNSTOK_L4_PROBE_AES_ONLY        // timing probe: no HMAC (wrong tags)
                     uint32_t w[16];
@@ -660,8 +634,7 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
                     st16(T, u32x4{bswap(tag[0]), bswap(tag[1]), bswap(tag[2]), bswap(tag[3])});
                     st16(T + 16, u32x4{bswap(tag[4]), bswap(tag[5]), bswap(tag[6]), bswap(tag[7])});
                 }
-              }
-              __syncthreads();
+                __syncthreads();
             }
         }
     }

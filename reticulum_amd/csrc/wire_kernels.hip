@@ -180,23 +180,6 @@ __device__ __forceinline__ void fill_sel_tables(SelTables *t) {
 __device__ __forceinline__ uint32_t byte_pattern(uint32_t m) {
     return ((((m >> 7) & 0x01010101u) * 0x01020408u) >> 24) & 0xFu;
 }
-#if defined(RNSTOK_FRAME_WORD_STORES) || defined(RNSTOK_UNESC_WORD_STORES)
-__device__ __forceinline__ void st4u(uint8_t *p, uint32_t v) { __builtin_memcpy(p, &v, 4); }
-// exactly n (0..8) bytes of lo||hi at q: whole dwords where they fit, bytes for the rest
-__device__ __forceinline__ void st_exact8(uint8_t *q, uint32_t lo, uint32_t hi, uint32_t n) {
-    if (n >= 4u) {
-        st4u(q, lo);
-        q += 4;
-        n -= 4u;
-        lo = hi;
-    }
-    if (n == 4u) {
-        st4u(q, lo);
-        return;
-    }
-    for (uint32_t t = 0; t < n; ++t) q[t] = (uint8_t)(lo >> (8 * t));
-}
-#endif
 
 // exactly k (0..16) bytes of lo||hi at d: a 16-B store, or 8/4/2/1-byte pieces
 __device__ __forceinline__ void st_exact16(uint8_t *d, uint64_t lo, uint64_t hi, uint32_t k) {
@@ -277,7 +260,6 @@ __global__ __launch_bounds__(256) void k_hdlc_write(const uint8_t *pkt, const ui
             const uint32_t sz = nb + esc;
             const uint32_t incl = row_incl_scan16(sz);
             uint8_t *q = o + base + (incl - sz);
-#ifndef RNSTOK_FRAME_WORD_STORES
             // HDLC.escape (TCPInterface.py:50-52: ESC first, then FLAG; per
             // byte the same: 7D x^0x20): each word expands through one
             // selector pair into 4..8 bytes; the lane's sz expanded bytes are
@@ -285,8 +267,9 @@ __global__ __launch_bounds__(256) void k_hdlc_write(const uint8_t *pkt, const ui
             // unescape: 16 B at q, and the rest (sz - 16 bytes) completed with
             // the next lane's first output bytes, which that lane stores too
             // with the same values; the row's last lane and a packet's last
-            // lane store exactly.  (RNSTOK_FRAME_WORD_STORES: every word of an
-            // escaping lane stored as a dword plus single bytes.)
+            // lane store exactly.  (The per-word form, every word of an escaping
+            // lane stored as a dword plus single bytes, was 6 % slower:
+            // profiles/r03x_frame_ab/.)
             uint64_t a[4] = {((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z, 0ull, 0ull};
             if (esc) {
                 const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
@@ -323,29 +306,6 @@ __global__ __launch_bounds__(256) void k_hdlc_write(const uint8_t *pkt, const ui
             } else if (sz) {
                 st_exact16(q, a[0], a[1], sz);
             }
-#else
-            if (esc == 0 && nb == 16) {
-                st16(q, v);
-            } else if (nb) {
-                // HDLC.escape (TCPInterface.py:50-52: ESC first, then FLAG; per
-                // byte the same: 7D x^0x20): each word expands through one
-                // selector pair into 4..8 bytes, stored exactly
-                const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-                uint32_t wpos = 0;
-#pragma unroll
-                for (uint32_t j = 0; j < 4; ++j) {
-                    if (4u * j < nb) {
-                        const uint32_t e = escbytes(wv[j]);            // bytes past nb are 0: never escapes
-                        const uint32_t pat = byte_pattern(e);
-                        const uint32_t x = wv[j] ^ (e >> 2);           // 0x80 -> 0x20 in the escaped bytes
-                        const uint32_t cnt = min(4u, nb - 4u * j) + __builtin_popcount(e);
-                        st_exact8(q + wpos, __builtin_amdgcn_perm(x, 0x7D7D7D7Du, tab.expand[pat][0]),
-                                  __builtin_amdgcn_perm(x, 0x7D7D7D7Du, tab.expand[pat][1]), cnt);
-                        wpos += cnt;
-                    }
-                }
-            }
-#endif
             base += row_sum16(sz);
         }
         if (rl == 0 && valid) o[base] = FLAG;
@@ -391,7 +351,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     return x + (lane >= 16u ? r0 : 0u) + (lane >= 32u ? r1 : 0u) + (lane >= 48u ? r2 : 0u);
 }
 
-#ifndef RNSTOK_FLAG_SCATTER_SPANS
 // Flag positions in stream order.  cnt_off + part: the chunk counts' scan
 // within blocks of SCAN_BLOCK chunks and the blocks' scanned totals (the
 // scan's third launch, adding the two, is folded in here).  Thread t loads the 16-B units t, t+256,
@@ -401,8 +360,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 // in its own quarter: the four per-thread counts (<= 16 each, <= 4096 per
 // block) ride as 16-bit fields of two words through one wave scan each and
 // one LDS exchange of the wave totals.  The form with 64 contiguous bytes
-// per thread (RNSTOK_FLAG_SCATTER_SPANS) loaded at a 64-B lane stride and
-// ranked with an 8-step LDS scan (16 barriers).
+// per thread loaded at a 64-B lane stride and ranked with an 8-step LDS scan
+// (16 barriers): 137 against 111 us, profiles/r03t_deframe_ab/.
 __global__ __launch_bounds__(256) void k_flag_scatter(const uint8_t *buf, uint64_t len, const uint64_t *cnt_off,
                                                       const uint64_t *part, uint64_t *pos) {
     const uint64_t cbase = (uint64_t)blockIdx.x * FLAG_CHUNK;
@@ -450,36 +409,6 @@ __global__ __launch_bounds__(256) void k_flag_scatter(const uint8_t *buf, uint64
         before += tot[k];
     }
 }
-#else
-// flag positions in stream order: thread t owns bytes [64t, 64t+64) of its chunk
-__global__ __launch_bounds__(256) void k_flag_scatter(const uint8_t *buf, uint64_t len, const uint64_t *cnt_off,
-                                                      const uint64_t *part, uint64_t *pos) {
-    const uint64_t base = (uint64_t)blockIdx.x * FLAG_CHUNK + threadIdx.x * 64ull;
-    uint32_t m[16], c = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-        const u32x4 v = base + 16 * k < len ? ld16_upto(buf, base + 16 * k, len) : u32x4{0u, 0u, 0u, 0u};
-        m[4 * k] = eqbytes(v.x, 0x7E7E7E7Eu); m[4 * k + 1] = eqbytes(v.y, 0x7E7E7E7Eu);
-        m[4 * k + 2] = eqbytes(v.z, 0x7E7E7E7Eu); m[4 * k + 3] = eqbytes(v.w, 0x7E7E7E7Eu);
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < 16; ++k) c += __builtin_popcount(m[k]);
-    // in-order rank of this thread's flags inside the chunk
-    __shared__ uint32_t sh[256];
-    sh[threadIdx.x] = c;
-    __syncthreads();
-    for (uint32_t d = 1; d < 256; d <<= 1) {
-        const uint32_t add = threadIdx.x >= d ? sh[threadIdx.x - d] : 0;
-        __syncthreads();
-        sh[threadIdx.x] += add;
-        __syncthreads();
-    }
-    if (c == 0) return;
-    uint64_t w = cnt_off[blockIdx.x] + part[blockIdx.x / SCAN_BLOCK] + sh[threadIdx.x] - c;
-    for (uint32_t k = 0; k < 16; ++k)
-        for (uint32_t f = m[k]; f; f &= f - 1) pos[w++] = base + 4 * k + (__builtin_ctz(f) >> 3);
-}
-#endif
 
 // One DPP row (16 lanes x 16 B) per consecutive flag pair (k, k+1), 4 pairs
 // per wave: the read loop's frame buf[pos_k+1 : pos_{k+1}) with its two
@@ -523,7 +452,6 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, uint6
         for (uint64_t w = a; w < e; w += 256u) {
             const uint64_t b = w + 16u * rl;
             const uint32_t nb = b < e ? (uint32_t)min((uint64_t)16, e - b) : 0u;
-#ifndef RNSTOK_UNESC_BYTE_TAIL
             // a window's last lane: one 16-B load with the bytes past the
             // frame masked off, unless the load would run past the stream
             // (the byte-wise form issues up to 15 loads one after another)
@@ -543,9 +471,6 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, uint6
             } else if (nb) {
                 v = ld16_upto(buf, b, e);
             }
-#else
-            const u32x4 v = nb ? ld16_upto(buf, b, e) : u32x4{0u, 0u, 0u, 0u};
-#endif
             uint32_t prevb = dpp<0x111>(v.w) >> 24;          // row_shr:1: the previous lane's last byte
             if (rl == 0) prevb = carry;
             uint32_t nextb = dpp<0x101>(v.x) & 0xFFu;         // row_shl:1: the next lane's first byte
@@ -553,7 +478,6 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, uint6
             if (rl == 15) nextb = b + 16 < e ? buf[b + 16] : 0u;
             const uint32_t x[4] = {v.x, v.y, v.z, v.w};
             uint32_t y[4], drop[4], ndrop = 0;
-#ifndef RNSTOK_UNESC_SHIFTED_WORDS
             // Each byte test once per word (7D, 5E, 5D: 0x80 per matching
             // byte), the neighbour's test by shifting the FLAG words by one
             // byte across the word and lane edges (the byte before the lane's
@@ -576,21 +500,9 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, uint6
                 y[j] = x[j] ^ ((conv >> 7) * 3u);                                                     // 7D -> 7E
                 ndrop += __builtin_popcount(drop[j]);
             }
-#else
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t pw = __builtin_amdgcn_alignbit(x[j], j ? x[j - 1] : prevb << 24, 24);   // previous bytes
-                const uint32_t nw = __builtin_amdgcn_alignbit(j < 3 ? x[j + 1] : nextb, x[j], 8);      // next bytes
-                drop[j] = eqbytes(pw, 0x7D7D7D7Du) & (eqbytes(x[j], 0x5E5E5E5Eu) | eqbytes(x[j], 0x5D5D5D5Du));
-                const uint32_t conv = eqbytes(x[j], 0x7D7D7D7Du) & eqbytes(nw, 0x5E5E5E5Eu);
-                y[j] = x[j] ^ ((conv >> 7) * 3u);                                                     // 7D -> 7E
-                ndrop += __builtin_popcount(drop[j]);
-            }
-#endif
             const uint32_t kept = nb - ndrop;
             const uint32_t incl = row_incl_scan16(kept);
             uint8_t *q = o + kept_total + (incl - kept);
-#ifndef RNSTOK_UNESC_WORD_STORES
             // Row-wide 16-B stores.  The lane's kept bytes are packed low in
             // c[0..3] (each word through its compaction selector, the pieces
             // placed with 64-bit shifts).  A lane then stores 16 bytes at its
@@ -600,8 +512,8 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, uint6
             // is written.  Lanes that cannot borrow enough from their
             // neighbour (the row's last lane, the frame's last lane, lanes
             // with fewer than 8 kept bytes) store exactly their bytes.  The
-            // per-word form (RNSTOK_UNESC_WORD_STORES) stored every word of an
-            // escape-holding lane as a dword plus single bytes.
+            // per-word form stored every word of an escape-holding lane as a dword
+            // plus single bytes: 459 against 368 us, profiles/r03s_unesc_ab/.
             uint32_t c[4] = {y[0], y[1], y[2], y[3]};
             if (kept != 16u) {
                 uint64_t lo = 0, hi = 0;
@@ -651,24 +563,6 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, uint6
                 }
                 if (k) *d = (uint8_t)v64;
             }
-#else
-            if (ndrop == 0 && nb == 16) {
-                st16(q, u32x4{y[0], y[1], y[2], y[3]});
-            } else if (nb) {
-                // each word's kept bytes through one compaction selector, stored exactly
-                uint32_t t = 0;
-#pragma unroll
-                for (uint32_t j = 0; j < 4; ++j) {
-                    if (4u * j < nb) {
-                        const uint32_t m = min(4u, nb - 4u * j);
-                        const uint32_t keep = byte_pattern(~drop[j] & 0x80808080u) & ((1u << m) - 1u);
-                        const uint32_t cnt = __builtin_popcount(keep);
-                        st_exact8(q + t, __builtin_amdgcn_perm(y[j], 0u, tab.compact[keep]), 0u, cnt);
-                        t += cnt;
-                    }
-                }
-            }
-#endif
             kept_total += row_sum16(kept);
             carry = row_sum16(rl == 15 ? v.w >> 24 : 0u);      // the window's last byte, to every lane
         }

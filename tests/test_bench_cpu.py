@@ -152,7 +152,8 @@ def test_committed_n_gt_1_lines_carry_every_north_star_number():
         assert n >= 2 and rec["value"] > 0 and rec["scaling"] == "weak"
         agg = rec["e2e_pcie"]["aggregate"]
         assert agg["ranks"] == n
-        for leg in ("serial", "pipelined"):
+        legs = ("serial", "pipelined") + (("pipelined_copy_engine",) if "pipelined_copy_engine" in agg else ())
+        for leg in legs:
             assert agg[leg]["ok_all"] is True and agg[leg]["encrypt_packets_s"] > 0 and agg[leg]["decrypt_packets_s"] > 0
         cpu = rec["cpu_baseline"]
         assert cpu["kind"] == "port" and cpu["value"] > 0 and cpu["cores"] >= 1

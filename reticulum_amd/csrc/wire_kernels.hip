@@ -14,7 +14,7 @@
 //   k_scan_*         exclusive prefix sums (u64) for frame placement
 //   k_hdlc_count     escaped frame length per packet
 //   k_hdlc_write     7E || escape(packet) || 7E at its prefix-sum offset
-//   k_flag_count / k_flag_scatter   positions of every 7E in a stream
+//   k_flag_local / k_flag_gather    positions of every 7E in a stream
 //   k_hdlc_unescape  one lane per consecutive flag pair: the read loop's two
 //                    bytes.replace passes, check_frame_len, empty-frame skip
 //   k_ifac           mask (outbound) / unmask (inbound) with HKDF(ifac, ifac_key)
@@ -316,31 +316,6 @@ __global__ __launch_bounds__(256) void k_hdlc_write(const uint8_t *pkt, const ui
 
 constexpr uint32_t FLAG_CHUNK = 16384;       // stream bytes per workgroup (256 threads x 64)
 
-// 0x80 per byte of the four words equal to c4
-__device__ __forceinline__ uint32_t flags16(u32x4 v) {
-    return __builtin_popcount(eqbytes(v.x, 0x7E7E7E7Eu)) + __builtin_popcount(eqbytes(v.y, 0x7E7E7E7Eu)) +
-           __builtin_popcount(eqbytes(v.z, 0x7E7E7E7Eu)) + __builtin_popcount(eqbytes(v.w, 0x7E7E7E7Eu));
-}
-
-// flags per chunk; each load instruction covers 1 KiB contiguous across the
-// workgroup's threads (the count does not depend on the order)
-__global__ __launch_bounds__(256) void k_flag_count(const uint8_t *buf, uint64_t len, uint64_t *cnt) {
-    const uint64_t base = (uint64_t)blockIdx.x * FLAG_CHUNK + threadIdx.x * 16ull;
-    uint32_t c = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < FLAG_CHUNK / 4096u; ++k) {
-        const uint64_t q = base + 4096ull * k;
-        if (q < len) c += flags16(ld16_upto(buf, q, len));
-    }
-    c = row_sum16(c);
-    __shared__ uint32_t s;
-    if (threadIdx.x == 0) s = 0;
-    __syncthreads();
-    if ((threadIdx.x & 15u) == 0) atomicAdd(&s, c);
-    __syncthreads();
-    if (threadIdx.x == 0) cnt[blockIdx.x] = s;
-}
-
 // wave-wide inclusive prefix sum: row scans, then the lower rows' totals
 // (readlane) added in
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
@@ -351,19 +326,18 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     return x + (lane >= 16u ? r0 : 0u) + (lane >= 32u ? r1 : 0u) + (lane >= 48u ? r2 : 0u);
 }
 
-// Flag positions in stream order.  cnt_off + part: the chunk counts' scan
-// within blocks of SCAN_BLOCK chunks and the blocks' scanned totals (the
-// scan's third launch, adding the two, is folded in here).  Thread t loads the 16-B units t, t+256,
-// t+512, t+768 of its chunk (each load instruction 1 KiB contiguous across a
-// wave, as k_flag_count); the stream-order rank of a unit's flags is the
+// Flag positions within each chunk, in stream order, and the chunk's flag
+// count: the one pass over the stream (k_flag_gather places them once the
+// counts are scanned; a separate counting pass read the stream a second
+// time).  Thread t loads the 16-B units t, t+256, t+512, t+768 of its chunk
+// (each load instruction 1 KiB contiguous across a wave); the stream-order rank of a unit's flags is the
 // block's flags in the earlier 4 KiB quarters plus those of the lower threads
 // in its own quarter: the four per-thread counts (<= 16 each, <= 4096 per
 // block) ride as 16-bit fields of two words through one wave scan each and
 // one LDS exchange of the wave totals.  The form with 64 contiguous bytes
 // per thread loaded at a 64-B lane stride and ranked with an 8-step LDS scan
 // (16 barriers): 137 against 111 us, profiles/r03t_deframe_ab/.
-__global__ __launch_bounds__(256) void k_flag_scatter(const uint8_t *buf, uint64_t len, const uint64_t *cnt_off,
-                                                      const uint64_t *part, uint64_t *pos) {
+__global__ __launch_bounds__(256) void k_flag_local(const uint8_t *buf, uint64_t len, uint64_t *cnt, uint16_t *loc) {
     const uint64_t cbase = (uint64_t)blockIdx.x * FLAG_CHUNK;
     const uint32_t t = threadIdx.x, wave = t >> 6;
     uint32_t m[4][4], c[4];
@@ -396,18 +370,32 @@ __global__ __launch_bounds__(256) void k_flag_scatter(const uint8_t *buf, uint64
     const uint32_t elo = plo + ilo - lo, ehi = phi + ihi - hi;
     const uint32_t excl[4] = {elo & 0xFFFFu, elo >> 16, ehi & 0xFFFFu, ehi >> 16};
     const uint32_t tot[4] = {tlo & 0xFFFFu, tlo >> 16, thi & 0xFFFFu, thi >> 16};
-    const uint64_t base = cnt_off[blockIdx.x] + part[blockIdx.x / SCAN_BLOCK];
+    uint16_t *out = loc + (uint64_t)blockIdx.x * FLAG_CHUNK;
+    if (t == 0) cnt[blockIdx.x] = tot[0] + tot[1] + tot[2] + tot[3];
     uint32_t before = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
         if (c[k]) {
-            uint64_t w = base + before + excl[k];
-            const uint64_t u = cbase + 4096ull * k + 16ull * t;
+            uint32_t w = before + excl[k];
+            const uint32_t u = 4096u * k + 16u * t;
             for (uint32_t j = 0; j < 4; ++j)
-                for (uint32_t f = m[k][j]; f; f &= f - 1) pos[w++] = u + 4 * j + (__builtin_ctz(f) >> 3);
+                for (uint32_t f = m[k][j]; f; f &= f - 1) out[w++] = (uint16_t)(u + 4 * j + (__builtin_ctz(f) >> 3));
         }
         before += tot[k];
     }
+}
+
+// Stream-order flag positions: chunk c's count[c] local positions (from
+// k_flag_local) go to pos[cnt_off[c] + part[c / SCAN_BLOCK] ...], one wave per
+// chunk.
+__global__ __launch_bounds__(256) void k_flag_gather(const uint64_t *cnt, const uint64_t *cnt_off, const uint64_t *part,
+                                                     const uint16_t *loc, uint64_t chunks, uint64_t *pos) {
+    const uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (c >= chunks) return;
+    const uint32_t lane = threadIdx.x & 63u, n = (uint32_t)cnt[c];
+    const uint64_t base = cnt_off[c] + part[c / SCAN_BLOCK], cb = c * FLAG_CHUNK;
+    const uint16_t *l = loc + cb;
+    for (uint32_t i = lane; i < n; i += 64u) pos[base + i] = cb + l[i];
 }
 
 // One DPP row (16 lanes x 16 B) per consecutive flag pair (k, k+1), 4 pairs
@@ -887,7 +875,7 @@ hipError_t launch_hdlc_frame(const uint8_t *pkt, const uint64_t *off, const uint
 
 uint64_t hdlc_deframe_workspace_bytes(uint64_t len) {
     const uint64_t chunks = (len + FLAG_CHUNK - 1) / FLAG_CHUNK;
-    return 8ull * chunks * 2 + scan_workspace_bytes(chunks) + 8ull * (len + 1) + 64;
+    return 8ull * chunks * 2 + scan_workspace_bytes(chunks) + 8ull * (len + 1) + 64 + 2ull * FLAG_CHUNK * chunks;
 }
 
 hipError_t launch_hdlc_deframe(const uint8_t *buf, uint64_t len, uint32_t hw_mtu, uint32_t ifac_size, uint8_t *out,
@@ -900,16 +888,18 @@ hipError_t launch_hdlc_deframe(const uint8_t *buf, uint64_t len, uint32_t hw_mtu
     // part[nb] receives the scanned total (k_scan_parts): the flag count
     uint64_t *nflags = part + (chunks + SCAN_BLOCK - 1) / SCAN_BLOCK;
     uint64_t *pos = nflags + 2;
+    uint16_t *loc = (uint16_t *)(pos + len + 1);         // chunk-local positions (k_flag_local)
     hipError_t e;
     if (!chunks && (e = hipMemsetAsync(nflags, 0, 8, s)) != hipSuccess) return e;   // else k_scan_parts writes it
     if (chunks) {
-        hipLaunchKernelGGL(k_flag_count, dim3((unsigned)chunks), dim3(256), 0, s, buf, len, cnt);
+        hipLaunchKernelGGL(k_flag_local, dim3((unsigned)chunks), dim3(256), 0, s, buf, len, cnt, loc);
         // chunk counts scanned within blocks, then the block totals (part[nb] = the flag count);
-        // the scatter adds the two
+        // the gather adds the two
         const uint64_t nb = (chunks + SCAN_BLOCK - 1) / SCAN_BLOCK;
         hipLaunchKernelGGL(k_scan_block, dim3((unsigned)nb), dim3(SCAN_BLOCK), 0, s, cnt, cnt_off, part, chunks);
         hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(SCAN_BLOCK), 0, s, part, nb);
-        hipLaunchKernelGGL(k_flag_scatter, dim3((unsigned)chunks), dim3(256), 0, s, buf, len, cnt_off, part, pos);
+        hipLaunchKernelGGL(k_flag_gather, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, s, cnt, cnt_off, part, loc,
+                           chunks, pos);
     }
     // the pair count lives on the device: a grid-stride kernel sized by the caller's capacity
     if (max_pairs) {

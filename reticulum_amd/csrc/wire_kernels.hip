@@ -825,19 +825,35 @@ __global__ __launch_bounds__(256) void k_unpack(const uint8_t *pkt, const uint64
     out[i] = f;
 }
 
+// Header bytes from registers: the 16-B fields are loaded whole and shifted by
+// two bytes across words (v_alignbit), so a HEADER_1 is one 16-B store plus
+// 2 + 1 bytes (HEADER_2: two 16-B stores plus 2 + 1); storing byte by byte
+// took 217 us for 2^20 headers (profiles/r03ab_node/).  The bytes after the
+// header (the packet's token, already in place) are not touched.
+__device__ __forceinline__ u32x4 shift_in2(uint32_t lo2, u32x4 d) {
+    // lo2 (2 bytes) || d[0..13]
+    return u32x4{(lo2 & 0xFFFFu) | (d.x << 16), __builtin_amdgcn_alignbit(d.y, d.x, 16),
+                 __builtin_amdgcn_alignbit(d.z, d.y, 16), __builtin_amdgcn_alignbit(d.w, d.z, 16)};
+}
 __global__ __launch_bounds__(256) void k_pack_headers(PackArgs a) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
     uint8_t *o = a.out + a.out_off[i];
-    o[0] = a.flags[i];
-    o[1] = a.hops ? a.hops[i] : 0;
-    uint32_t w = 2;
+    const uint32_t fh = (uint32_t)a.flags[i] | (a.hops ? (uint32_t)a.hops[i] << 8 : 0u);
+    const u32x4 dh = ld16(a.destination_hash + 16ull * i);
+    u32x4 last = dh;                                    // the field whose bytes 14, 15 end the header
     if (a.transport_id) {
-        for (int k = 0; k < 16; ++k) o[w + k] = a.transport_id[16ull * i + k];
-        w += 16;
+        const u32x4 tid = ld16(a.transport_id + 16ull * i);
+        st16(o, shift_in2(fh, tid));
+        st16(o + 16, shift_in2(tid.w >> 16, dh));
+        o += 32;
+    } else {
+        st16(o, shift_in2(fh, dh));
+        o += 16;
     }
-    for (int k = 0; k < 16; ++k) o[w + k] = a.destination_hash[16ull * i + k];
-    o[w + 16] = a.context[i];
+    const uint16_t t2 = (uint16_t)(last.w >> 16);
+    __builtin_memcpy(o, &t2, 2);
+    o[2] = a.context[i];
 }
 
 }  // namespace

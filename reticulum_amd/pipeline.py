@@ -1,0 +1,135 @@
+"""A Reticulum interface's packet path, device-resident end to end
+("what surrounds the token on the interface path ... needed
+for a true end-to-end node pipeline").
+
+Outbound, as a node sends DATA packets through an interface with IFAC:
+    Token.encrypt            Token.py:87-97 (Packet.pack -> Destination/Link.encrypt)
+    Packet.pack header       Packet.py:178-228
+    IFAC mask                Transport.py:1069-1101 (transmit)
+    HDLC framing             TCPInterface.py:44-53, 323 (process_outgoing)
+Inbound, as the interface's read loop hands frames to Transport:
+    HDLC deframing           TCPInterface.py:387-410 (read_loop)
+    IFAC unmask              Transport.py:1441-1475 (inbound; the Ed25519
+                             signature check that follows, :1477-1481, stays
+                             with the caller: `ifac` is returned for it)
+    Packet.unpack + hash     Packet.py:242-275, 342-353
+    Token.decrypt            Token.py:100-114 (Link/Identity.decrypt)
+
+Every stage is one of reticulum_amd.device's kernels; between them only
+offsets and lengths are rearranged (torch plumbing on the same stream), and
+nothing is synchronised: sizes the host does not know (the number of frames
+in a stream) stay on the device, and entries past them carry length 0, which
+every later stage rejects like the reference does (a frame too short for its
+IFAC, a packet too short for its header, a token too short for its tag).
+"""
+import torch
+
+from . import device
+from .token import KeySet, token_len
+
+HEADER_1_LEN = 19           # flags, hops, destination hash (16), context: Packet.py:178-228
+FRAME_OK = 0                # RT_FRAME_OK (include/rnstok.h)
+
+
+def outbound(ks: KeySet, pt, iv, destination_hash, context, ifac, ifac_key, flags=None, hops=None, stream=None):
+    """n DATA packets of one length L, one link key: pt (n, L) uint8, iv (n,
+    16), destination_hash (n, 16), context (n,) uint8, flags/hops (n,) uint8
+    (default 0: HEADER_1 DATA, hop 0), ifac (n, ifac_size) the access codes
+    (the tail of the interface identity's signature of each packet, made by
+    the caller), ifac_key (K,) uint8.  Returns (stream, frame_off): the HDLC
+    byte stream is stream[:frame_off[n]] (int64 on the device), frame i at
+    stream[frame_off[i]:frame_off[i+1]]."""
+    n, L = pt.shape
+    dev = pt.device
+    flags = flags if flags is not None else torch.zeros(n, dtype=torch.uint8, device=dev)
+    hops = hops if hops is not None else torch.zeros(n, dtype=torch.uint8, device=dev)
+    pl = HEADER_1_LEN + token_len(L)
+    raw = torch.empty((n, pl), dtype=torch.uint8, device=dev)
+    device.encrypt_uniform(ks, pt, L, iv, raw[:, HEADER_1_LEN:], stream=stream)
+    off = torch.arange(n, dtype=torch.int64, device=dev) * pl
+    flat = raw.view(-1)
+    device.pack_headers(flags, hops, destination_hash, context, flat, off, stream=stream)
+    isz = ifac.shape[1]
+    ml = pl + isz
+    masked = torch.empty(n * ml, dtype=torch.uint8, device=dev)
+    m_off = torch.arange(n, dtype=torch.int64, device=dev) * ml
+    device.ifac_mask(flat, off, torch.full((n,), pl, dtype=torch.int32, device=dev), ifac, ifac_key, masked, m_off,
+                     stream=stream)
+    framed = torch.empty(n * (2 * ml + 2), dtype=torch.uint8, device=dev)
+    frame_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    device.hdlc_frame(masked, m_off, torch.full((n,), ml, dtype=torch.int32, device=dev), framed, frame_off,
+                      stream=stream)
+    return framed, frame_off
+
+
+def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stream=None):
+    """One read of an interface's byte stream ``buf`` (uint8 on the device)
+    through deframing, IFAC unmask, unpack and token decrypt, for at most
+    ``max_pairs`` consecutive flag pairs (a stream of n frames has 2n - 1:
+    frames and the empty gaps between them).
+
+    Returns a dict of device tensors.  Per flag pair k: ``frame_status``
+    (RT_FRAME_*; -1 past the pairs found) and ``counts`` = [pairs, bytes
+    consumed] as the read loop leaves them (TCPInterface.py:391-411).  The
+    frames the read loop hands on (RT_FRAME_OK) are compacted in stream order
+    into the first ``n_frames`` (a device scalar) entries of the per-frame
+    arrays, whose remaining entries are empty: ``frame_pair`` (their pair
+    index), ``ifac_status`` (0: unmasked; 1: dropped before the signature
+    check), ``ifac`` (the access code for the caller's signature check),
+    ``fields`` (rt_packet_fields; ok = 0 where unpack fails), and the token's
+    outcome: ``status`` (RT_* token status; TOO_SHORT where there is no
+    packet) with the plaintext at ``pt[pt_off[i]: pt_off[i] + pt_len[i]]``.
+    Compacting first keeps the per-packet kernels' waves full (the gaps
+    between frames would otherwise be half of every wave)."""
+    dev = buf.device
+    out = torch.empty(buf.numel(), dtype=torch.uint8, device=dev)
+    d_off = torch.zeros(max_pairs, dtype=torch.int64, device=dev)
+    d_len = torch.zeros(max_pairs, dtype=torch.int32, device=dev)
+    d_st = torch.full((max_pairs,), -1, dtype=torch.int32, device=dev)
+    counts = torch.empty(2, dtype=torch.int64, device=dev)
+    device.hdlc_deframe(buf, out, d_off, d_len, d_st, counts, hw_mtu=hw_mtu, ifac_size=ifac_size, stream=stream)
+    with _on(stream):
+        ok = (torch.arange(max_pairs, device=dev) < counts[0]) & (d_st == FRAME_OK)
+        rank = torch.cumsum(ok, 0, dtype=torch.int64) - 1
+        n_frames = rank[-1] + 1 if max_pairs else torch.zeros((), dtype=torch.int64, device=dev)
+        # scatter the OK frames to the front; everything else lands in a dump slot past the end
+        idx = torch.where(ok, rank, torch.full_like(rank, max_pairs))
+        f_off = torch.zeros(max_pairs + 1, dtype=torch.int64, device=dev).scatter_(0, idx, d_off)[:max_pairs]
+        f_len = torch.zeros(max_pairs + 1, dtype=torch.int32, device=dev).scatter_(0, idx, d_len)[:max_pairs]
+        frame_pair = torch.full((max_pairs + 1,), -1, dtype=torch.int64, device=dev).scatter_(
+            0, idx, torch.arange(max_pairs, device=dev))[:max_pairs]
+        f_off, f_len = f_off.contiguous(), f_len.contiguous()
+    un = torch.empty_like(out)
+    ifac = torch.empty((max_pairs, ifac_size), dtype=torch.uint8, device=dev)
+    ifac_status = torch.empty(max_pairs, dtype=torch.int32, device=dev)
+    device.ifac_unmask(out, f_off, f_len, ifac_key, ifac, un, f_off, ifac_status, stream=stream)
+    with _on(stream):
+        p_len = torch.where(ifac_status == 0, f_len - ifac_size, torch.zeros_like(f_len)).contiguous()
+    fields = torch.empty((max_pairs, 96), dtype=torch.uint8, device=dev)
+    device.packet_unpack(un, f_off, p_len, fields, stream=stream)
+    with _on(stream):
+        words = fields.view(torch.int32)          # rt_packet_fields: data_offset, data_len at bytes 12..19
+        data_ok = fields[:, 0] == 1
+        tok_off = torch.where(data_ok, f_off + words[:, 3].to(torch.int64), f_off).contiguous()
+        tok_len = torch.where(data_ok, words[:, 4], torch.zeros_like(words[:, 4])).contiguous()
+    pt = torch.empty_like(un)
+    pt_len = torch.empty(max_pairs, dtype=torch.int32, device=dev)
+    status = torch.empty(max_pairs, dtype=torch.int32, device=dev)
+    # each plaintext (at most its token's length - 48 bytes) is written inside its own token's span
+    device.decrypt(ks, un, tok_off, tok_len, pt, tok_off, pt_len, status, stream=stream)
+    return {"pt": pt, "pt_off": tok_off, "pt_len": pt_len, "status": status, "ifac": ifac,
+            "ifac_status": ifac_status, "fields": fields, "frame_pair": frame_pair, "n_frames": n_frames,
+            "frame_status": d_st, "counts": counts}
+
+
+def _on(stream):
+    """torch plumbing on the pipeline's stream (the device calls take it explicitly)."""
+    return torch.cuda.stream(stream) if stream is not None else _null()
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

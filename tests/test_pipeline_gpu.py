@@ -1,0 +1,90 @@
+"""The interface path composed on the device (reticulum_amd.pipeline):
+outbound token encrypt -> header pack -> IFAC mask -> HDLC framing gives
+exactly the stream the reference's steps give (the oracle's restatements of
+Token.encrypt, Packet.pack, Transport.transmit and HDLC.escape, each pinned to
+reference-generated vectors), and inbound deframing -> IFAC unmask -> unpack
+-> token decrypt of that stream gives back every packet, its IFAC, header
+fields and plaintext; a tampered tag fails that packet alone."""
+import numpy as np
+import pytest
+
+from oracle import ctoken
+from oracle import wire as ow
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(n, L, isz, seed):
+    import torch
+    rng = np.random.Generator(np.random.PCG64(seed))
+    key = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+    ifac_key = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+    pt = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    iv = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    dh = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    ctx = rng.integers(0, 256, n, dtype=np.uint8)
+    ifac = rng.integers(0, 256, (n, isz), dtype=np.uint8)
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return key, ifac_key, pt, iv, dh, ctx, ifac, t
+
+
+def _reference_stream(key, ifac_key, pt, iv, dh, ctx, ifac):
+    frames = []
+    for i in range(pt.shape[0]):
+        tok = ctoken.encrypt(key, iv[i].tobytes(), pt[i].tobytes())
+        raw = ow.pack_header(0, 0, dh[i].tobytes(), int(ctx[i])) + tok
+        frames.append(ow.hdlc_frame(ow.ifac_mask(raw, ifac[i].tobytes(), ifac_key)))
+    return b"".join(frames)
+
+
+@pytest.mark.parametrize("n,L,isz", [(1500, 383, 16), (700, 17, 8), (257, 0, 16)])
+def test_outbound_stream_is_the_references_and_inbound_returns_every_packet(n, L, isz):
+    import torch
+    import reticulum_amd as rt
+    from reticulum_amd import pipeline
+    key, ifac_key, pt, iv, dh, ctx, ifac, t = _case(n, L, isz, 100 + n + L)
+    ks = rt.KeySet(key, device=0)
+    framed, foff = pipeline.outbound(ks, t(pt), t(iv), t(dh), t(ctx), t(ifac), t(np.frombuffer(ifac_key, np.uint8)))
+    total = int(foff[-1])
+    stream = framed[:total].cpu().numpy().tobytes()
+    assert stream == _reference_stream(key, ifac_key, pt, iv, dh, ctx, ifac)
+
+    res = pipeline.inbound(ks, framed[:total].clone(), t(np.frombuffer(ifac_key, np.uint8)), isz, 2 * n)
+    torch.cuda.synchronize()
+    assert int(res["n_frames"]) == n and int(res["counts"][0]) == 2 * n - 1
+    assert res["frame_pair"][:n].cpu().tolist() == list(range(0, 2 * n, 2))
+    assert bool((res["ifac_status"][:n] == 0).all()) and torch.equal(res["ifac"][:n].cpu(), torch.from_numpy(ifac))
+    f = res["fields"][:n].cpu().numpy()
+    assert (f[:, 0] == 1).all() and (f[:, 8] == ctx).all() and (f[:, 36:52] == dh).all()     # ok, context, destination
+    assert bool((res["status"][:n] == 0).all()) and bool((res["pt_len"][:n] == L).all())
+    p, po = res["pt"].cpu().numpy(), res["pt_off"][:n].cpu().numpy()
+    for i in range(n):
+        assert p[po[i]:po[i] + L].tobytes() == pt[i].tobytes(), i
+    # the entries past the frames carry nothing
+    assert bool((res["ifac_status"][n:] == 1).all()) and bool((res["status"][n:] == 1).all())
+
+
+def test_inbound_tampered_tag_fails_that_packet_alone():
+    import torch
+    import reticulum_amd as rt
+    from reticulum_amd import pipeline
+    n, L, isz = 400, 383, 16
+    key, ifac_key, pt, iv, dh, ctx, ifac, t = _case(n, L, isz, 77)
+    ks = rt.KeySet(key, device=0)
+    framed, foff = pipeline.outbound(ks, t(pt), t(iv), t(dh), t(ctx), t(ifac), t(np.frombuffer(ifac_key, np.uint8)))
+    buf = bytearray(framed[:int(foff[-1])].cpu().numpy().tobytes())
+    fo = foff.cpu().numpy()
+    hit = []
+    for i in (3, 150, 399):
+        p = int(fo[i + 1]) - 6                      # inside the last bytes of frame i: its HMAC tag
+        while buf[p] in (0x7D, 0x7E) or buf[p - 1] == 0x7D or (buf[p] ^ 1) in (0x7D, 0x7E):
+            p -= 1
+        buf[p] ^= 1
+        hit.append(i)
+    res = pipeline.inbound(ks, torch.frombuffer(bytes(buf), dtype=torch.uint8).to("cuda"),
+                           t(np.frombuffer(ifac_key, np.uint8)), isz, 2 * n)
+    st = res["status"][:n].cpu().numpy()
+    assert int(res["n_frames"]) == n
+    assert sorted(np.nonzero(st)[0].tolist()) == hit and all(st[i] == 2 for i in hit)      # RT_BAD_HMAC
+    assert bool((res["pt_len"][:n].cpu()[torch.from_numpy(st == 0)] == L).all())

@@ -86,6 +86,8 @@ def parse():
     ap.add_argument("--one-layout", action="store_true", help="time only --layout")
     ap.add_argument("--e2e", action="store_true", default=True, help="also time the PCIe-inclusive path")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false")
+    ap.add_argument("--no-node", dest="node", action="store_false",
+                    help="skip the composed interface path (reticulum_amd.pipeline) at N = 1")
     return ap.parse_args()
 
 
@@ -359,6 +361,12 @@ def main():
     # once on its own shard, over its own PCIe link (the node's host-origin rate)
     # (N > 1: below, after the headline line exists, under a deadline)
     e2e = e2e_rate(ks, pt, iv, L, tl, n, stream) if args.e2e and world == 1 else None
+    node = None
+    if args.node and world == 1 and args.config == "c2":
+        try:
+            node = node_rate(dev)
+        except Exception as exc:          # never fatal for the headline
+            node = {"error": f"{type(exc).__name__}: {exc}"}
 
     lib = _native.load()
     n_cu = lib.rt_num_cus(_native.context(local))
@@ -455,6 +463,7 @@ def main():
         "cpu_openssl": cpu_ssl,
         "other_layout": other,
         "e2e_pcie": e2e,
+        "node_pipeline": node,
         "sharded_c4": None,
     }
 
@@ -967,6 +976,63 @@ def traffic_from_profiles(kernel, n, L, keys, layout="rows"):
                                    "(tools/fetch_calib.hip, profiles/r01c_fetch_calib.txt), the encrypt kernel "
                                    "1.32x of its algorithmic reads: no over-fetch beyond the access pattern's own"}
     return None
+
+
+def node_rate(dev, steps=10, g=None, n=1 << 20, L=383, isz=16):
+    """The interface path composed on the device (reticulum_amd.pipeline,
+    DESIGN.md §4.8): n DATA packets of L B plaintext (383 B: a 432-B token,
+    451-B packet, 467 B with a 16-B IFAC) out through token encrypt -> header
+    pack -> IFAC mask -> HDLC framing into one stream, and that stream back in
+    through deframing -> IFAC unmask -> unpack -> token decrypt.  Median of
+    ``steps`` HIP-event timings per direction after the clock warmup; a
+    sample of 4096 plaintexts, every status and every IFAC checked."""
+    import torch
+    import reticulum_amd as rt
+    from reticulum_amd import pipeline
+    g = g if g is not None else torch.Generator(device=dev).manual_seed(6)
+    pt = torch.randint(0, 256, (n, L), dtype=torch.uint8, device=dev, generator=g)
+    iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
+    dh = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
+    ctx = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev, generator=g)
+    ifac = torch.randint(0, 256, (n, isz), dtype=torch.uint8, device=dev, generator=g)
+    ikey = torch.randint(0, 256, (64,), dtype=torch.uint8, device=dev, generator=g)
+    ks = rt.KeySet(bytes(range(64)), device=dev.index if dev.index is not None else 0)
+    state = {}
+
+    def outb():
+        state["framed"], state["foff"] = pipeline.outbound(ks, pt, iv, dh, ctx, ifac, ikey)
+
+    outb()
+    torch.cuda.synchronize()
+    total = int(state["foff"][-1])
+    stream_buf = state["framed"][:total].clone()
+
+    def inb():
+        state["res"] = pipeline.inbound(ks, stream_buf, ikey, isz, 2 * n)
+
+    inb()
+    torch.cuda.synchronize()
+    r = state["res"]
+    rows = torch.randint(0, n, (4096,), device=dev, generator=g)
+    idx = r["pt_off"][rows].unsqueeze(1) + torch.arange(L, device=dev)
+    ok = (int(r["n_frames"]) == n and bool((r["status"][:n] == 0).all()) and bool((r["pt_len"][:n] == L).all())
+          and torch.equal(r["pt"][idx], pt[rows]) and torch.equal(r["ifac"][:n], ifac))
+    res = {"packets": n, "plaintext_bytes": L, "ifac_size": isz, "stream_bytes": total, "ok": ok}
+    stream = torch.cuda.current_stream(dev)
+    for name, f in (("outbound", outb), ("inbound", inb)):
+        warmup(f, stream, 2, 0.3)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for a, b in ev:
+            a.record(stream)
+            f()
+            b.record(stream)
+        torch.cuda.synchronize()
+        ms = sorted(a.elapsed_time(b) for a, b in ev)[steps // 2]
+        res[name] = {"ms": ms, "packets_s": n / (ms * 1e-3), "stream_gb_s": total / (ms * 1e-3) / 1e9}
+    res["note"] = ("reticulum_amd.pipeline: outbound = token encrypt, Packet.pack header, IFAC mask, HDLC framing "
+                   "(one stream); inbound = HDLC deframing, IFAC unmask, Packet.unpack + hash, token decrypt; "
+                   "device-resident, one link key, synthetic payloads; DESIGN.md \u00a74.8")
+    return res
 
 
 def e2e_rate(ks, pt_dev, iv_dev, L, tl, n, stream, reps=3, chunks=32, n_streams=3, sync_all=None,

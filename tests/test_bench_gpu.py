@@ -34,3 +34,13 @@ def test_c3_key_setup_times():
     keys = np.random.default_rng(3).integers(0, 256, (4096, 64), dtype=np.uint8)
     r = bench.key_setup_times(keys, 0, torch.device("cuda", 0), reps=2)
     assert r["keys"] == 4096 and r["host_ms"] > 0 and r["device_ms"] > 0 and r["keys_per_s_device"] > 0
+
+
+def test_node_rate_small():
+    """bench.node_rate (the composed interface path in the bench line) at a
+    small size: both directions timed, every packet back."""
+    import torch
+    import bench
+    r = bench.node_rate(torch.device("cuda", 0), steps=3, n=4096)
+    assert r["ok"] is True and r["packets"] == 4096
+    assert r["outbound"]["ms"] > 0 and r["inbound"]["ms"] > 0 and r["stream_bytes"] > 4096 * 467

@@ -335,49 +335,8 @@ def resource_config(dev, g, steps):
 
 
 def node_config(dev, g, steps):
-    import torch
-    import reticulum_amd as rt
-    from reticulum_amd import pipeline
-    n, L, isz = 1 << 20, 383, 16
-    pt = torch.randint(0, 256, (n, L), dtype=torch.uint8, device=dev, generator=g)
-    iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
-    dh = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
-    ctx = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev, generator=g)
-    ifac = torch.randint(0, 256, (n, isz), dtype=torch.uint8, device=dev, generator=g)
-    ikey = torch.randint(0, 256, (64,), dtype=torch.uint8, device=dev, generator=g)
-    ks = rt.KeySet(bytes(range(64)), device=0)
-    state = {}
-
-    def outb():
-        state["framed"], state["foff"] = pipeline.outbound(ks, pt, iv, dh, ctx, ifac, ikey)
-
-    outb()
-    torch.cuda.synchronize()
-    total = int(state["foff"][-1])
-    stream_buf = state["framed"][:total].clone()
-
-    def inb():
-        state["res"] = pipeline.inbound(ks, stream_buf, ikey, isz, 2 * n)
-
-    inb()
-    torch.cuda.synchronize()
-    r = state["res"]
-    rows = torch.randint(0, n, (4096,), device=dev, generator=g)
-    idx = r["pt_off"][rows].unsqueeze(1) + torch.arange(L, device=dev)
-    ok = (int(r["n_frames"]) == n and bool((r["status"][:n] == 0).all()) and bool((r["pt_len"][:n] == L).all())
-          and torch.equal(r["pt"][idx], pt[rows]) and torch.equal(r["ifac"][:n], ifac))
-    res = {"config": "node", "packets": n, "plaintext_bytes": L, "ifac_size": isz, "stream_bytes": total, "ok": ok}
-    for name, f in (("outbound", outb), ("inbound", inb)):
-        warm(f)
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-        for a, b in ev:
-            a.record()
-            f()
-            b.record()
-        torch.cuda.synchronize()
-        ms = sorted(a.elapsed_time(b) for a, b in ev)[steps // 2]
-        res[name] = {"ms": ms, "packets_s": n / (ms * 1e-3), "stream_gb_s": total / (ms * 1e-3) / 1e9}
-    return res
+    import bench
+    return bench.node_rate(dev, steps, g)
 
 
 def wire_config(dev, g, steps):

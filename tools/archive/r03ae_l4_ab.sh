@@ -1,6 +1,6 @@
 #!/bin/bash
 # k_encrypt_long4: each lookup issued right after its address, in the order
-# the terms are used (RNSTOK_L4_INTERLEAVE, a macro of that commit only; build_exp/l4il) vs the compiler's
+# the terms are used (a variant built from a local edit of enc_block4 described in DESIGN.md §4.2 (d) and not kept; build_exp/l4il) vs the compiler's
 # grouping (build_exp/base); A/B in one process at the c4 8-GPU shard, one
 # Token-sized call and a 128-per-CU batch of 500-B packets.
 set -o pipefail

@@ -1404,8 +1404,15 @@ static hipError_t launch_enc_long_nr(const EncArgs &a, int n_cu, hipStream_t s) 
 #ifndef RNSTOK_LONG_PERKEY_MIN_LEN
 #define RNSTOK_LONG_PERKEY_MIN_LEN 0u
 #endif
+// Tokens per CU up to which the long-token kernels run (one persistent
+// workgroup of 128 chains per CU).  A build with a larger value forces them
+// onto big batches: the measured comparison of their lane-cooperative CBC
+// and wave-split HMAC with one packet per lane at c2.
+#ifndef RNSTOK_LONG_MAX_PER_CU
+#define RNSTOK_LONG_MAX_PER_CU 128ull
+#endif
 static bool use_long(uint32_t n, const uint32_t *len, uint32_t uni, int n_cu, uint32_t min_len) {
-    return len == nullptr && uni >= min_len && (uint64_t)n <= 128ull * (uint64_t)n_cu;
+    return len == nullptr && uni >= min_len && (uint64_t)n <= RNSTOK_LONG_MAX_PER_CU * (uint64_t)n_cu;
 }
 
 template <int NR>
@@ -1468,7 +1475,7 @@ int plan_decrypt(uint32_t n, bool packed, uint32_t uni_len, bool per_key, int n_
     // long mode: one key, uniform well-formed tokens (whole blocks, at least
     // one), few per CU
     if (!per_key && !packed && uni_len >= 64u && uni_len >= 48u + RNSTOK_LONG_MIN_LEN &&
-        ((uni_len - 48u) & 15u) == 0 && (uint64_t)n <= 128ull * (uint64_t)n_cu)
+        ((uni_len - 48u) & 15u) == 0 && (uint64_t)n <= RNSTOK_LONG_MAX_PER_CU * (uint64_t)n_cu)
         return RT_KERNEL_DEC_LONG2;
     return RT_KERNEL_GENERAL;
 }

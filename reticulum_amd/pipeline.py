@@ -21,7 +21,13 @@ nothing is synchronised: sizes the host does not know (the number of frames
 in a stream) stay on the device, and entries past them carry length 0, which
 every later stage rejects like the reference does (a frame too short for its
 IFAC, a packet too short for its header, a token too short for its tag).
+With ``stream`` given, every launch and every temporary is on that stream
+(allocated there, so the caching allocator never hands a temporary to other
+work before the stream is done with it) and so are the results: the caller
+makes its own stream wait on it before reading them.
 """
+import contextlib
+
 import torch
 
 from . import device
@@ -39,26 +45,27 @@ def outbound(ks: KeySet, pt, iv, destination_hash, context, ifac, ifac_key, flag
     the caller), ifac_key (K,) uint8.  Returns (stream, frame_off): the HDLC
     byte stream is stream[:frame_off[n]] (int64 on the device), frame i at
     stream[frame_off[i]:frame_off[i+1]]."""
-    n, L = pt.shape
-    dev = pt.device
-    flags = flags if flags is not None else torch.zeros(n, dtype=torch.uint8, device=dev)
-    hops = hops if hops is not None else torch.zeros(n, dtype=torch.uint8, device=dev)
-    pl = HEADER_1_LEN + token_len(L)
-    raw = torch.empty((n, pl), dtype=torch.uint8, device=dev)
-    device.encrypt_uniform(ks, pt, L, iv, raw[:, HEADER_1_LEN:], stream=stream)
-    off = torch.arange(n, dtype=torch.int64, device=dev) * pl
-    flat = raw.view(-1)
-    device.pack_headers(flags, hops, destination_hash, context, flat, off, stream=stream)
-    isz = ifac.shape[1]
-    ml = pl + isz
-    masked = torch.empty(n * ml, dtype=torch.uint8, device=dev)
-    m_off = torch.arange(n, dtype=torch.int64, device=dev) * ml
-    device.ifac_mask(flat, off, torch.full((n,), pl, dtype=torch.int32, device=dev), ifac, ifac_key, masked, m_off,
-                     stream=stream)
-    framed = torch.empty(n * (2 * ml + 2), dtype=torch.uint8, device=dev)
-    frame_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    device.hdlc_frame(masked, m_off, torch.full((n,), ml, dtype=torch.int32, device=dev), framed, frame_off,
-                      stream=stream)
+    with _on(stream):      # temporaries allocated on the stream that uses them
+        n, L = pt.shape
+        dev = pt.device
+        flags = flags if flags is not None else torch.zeros(n, dtype=torch.uint8, device=dev)
+        hops = hops if hops is not None else torch.zeros(n, dtype=torch.uint8, device=dev)
+        pl = HEADER_1_LEN + token_len(L)
+        raw = torch.empty((n, pl), dtype=torch.uint8, device=dev)
+        device.encrypt_uniform(ks, pt, L, iv, raw[:, HEADER_1_LEN:], stream=stream)
+        off = torch.arange(n, dtype=torch.int64, device=dev) * pl
+        flat = raw.view(-1)
+        device.pack_headers(flags, hops, destination_hash, context, flat, off, stream=stream)
+        isz = ifac.shape[1]
+        ml = pl + isz
+        masked = torch.empty(n * ml, dtype=torch.uint8, device=dev)
+        m_off = torch.arange(n, dtype=torch.int64, device=dev) * ml
+        device.ifac_mask(flat, off, torch.full((n,), pl, dtype=torch.int32, device=dev), ifac, ifac_key, masked, m_off,
+                         stream=stream)
+        framed = torch.empty(n * (2 * ml + 2), dtype=torch.uint8, device=dev)
+        frame_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        device.hdlc_frame(masked, m_off, torch.full((n,), ml, dtype=torch.int32, device=dev), framed, frame_off,
+                          stream=stream)
     return framed, frame_off
 
 
@@ -81,14 +88,14 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
     packet) with the plaintext at ``pt[pt_off[i]: pt_off[i] + pt_len[i]]``.
     Compacting first keeps the per-packet kernels' waves full (the gaps
     between frames would otherwise be half of every wave)."""
-    dev = buf.device
-    out = torch.empty(buf.numel(), dtype=torch.uint8, device=dev)
-    d_off = torch.zeros(max_pairs, dtype=torch.int64, device=dev)
-    d_len = torch.zeros(max_pairs, dtype=torch.int32, device=dev)
-    d_st = torch.full((max_pairs,), -1, dtype=torch.int32, device=dev)
-    counts = torch.empty(2, dtype=torch.int64, device=dev)
-    device.hdlc_deframe(buf, out, d_off, d_len, d_st, counts, hw_mtu=hw_mtu, ifac_size=ifac_size, stream=stream)
-    with _on(stream):
+    with _on(stream):      # temporaries allocated on the stream that uses them
+        dev = buf.device
+        out = torch.empty(buf.numel(), dtype=torch.uint8, device=dev)
+        d_off = torch.zeros(max_pairs, dtype=torch.int64, device=dev)
+        d_len = torch.zeros(max_pairs, dtype=torch.int32, device=dev)
+        d_st = torch.full((max_pairs,), -1, dtype=torch.int32, device=dev)
+        counts = torch.empty(2, dtype=torch.int64, device=dev)
+        device.hdlc_deframe(buf, out, d_off, d_len, d_st, counts, hw_mtu=hw_mtu, ifac_size=ifac_size, stream=stream)
         ok = (torch.arange(max_pairs, device=dev) < counts[0]) & (d_st == FRAME_OK)
         rank = torch.cumsum(ok, 0, dtype=torch.int64) - 1
         n_frames = rank[-1] + 1 if max_pairs else torch.zeros((), dtype=torch.int64, device=dev)
@@ -99,24 +106,22 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
         frame_pair = torch.full((max_pairs + 1,), -1, dtype=torch.int64, device=dev).scatter_(
             0, idx, torch.arange(max_pairs, device=dev))[:max_pairs]
         f_off, f_len = f_off.contiguous(), f_len.contiguous()
-    un = torch.empty_like(out)
-    ifac = torch.empty((max_pairs, ifac_size), dtype=torch.uint8, device=dev)
-    ifac_status = torch.empty(max_pairs, dtype=torch.int32, device=dev)
-    device.ifac_unmask(out, f_off, f_len, ifac_key, ifac, un, f_off, ifac_status, stream=stream)
-    with _on(stream):
+        un = torch.empty_like(out)
+        ifac = torch.empty((max_pairs, ifac_size), dtype=torch.uint8, device=dev)
+        ifac_status = torch.empty(max_pairs, dtype=torch.int32, device=dev)
+        device.ifac_unmask(out, f_off, f_len, ifac_key, ifac, un, f_off, ifac_status, stream=stream)
         p_len = torch.where(ifac_status == 0, f_len - ifac_size, torch.zeros_like(f_len)).contiguous()
-    fields = torch.empty((max_pairs, 96), dtype=torch.uint8, device=dev)
-    device.packet_unpack(un, f_off, p_len, fields, stream=stream)
-    with _on(stream):
+        fields = torch.empty((max_pairs, 96), dtype=torch.uint8, device=dev)
+        device.packet_unpack(un, f_off, p_len, fields, stream=stream)
         words = fields.view(torch.int32)          # rt_packet_fields: data_offset, data_len at bytes 12..19
         data_ok = fields[:, 0] == 1
         tok_off = torch.where(data_ok, f_off + words[:, 3].to(torch.int64), f_off).contiguous()
         tok_len = torch.where(data_ok, words[:, 4], torch.zeros_like(words[:, 4])).contiguous()
-    pt = torch.empty_like(un)
-    pt_len = torch.empty(max_pairs, dtype=torch.int32, device=dev)
-    status = torch.empty(max_pairs, dtype=torch.int32, device=dev)
-    # each plaintext (at most its token's length - 48 bytes) is written inside its own token's span
-    device.decrypt(ks, un, tok_off, tok_len, pt, tok_off, pt_len, status, stream=stream)
+        pt = torch.empty_like(un)
+        pt_len = torch.empty(max_pairs, dtype=torch.int32, device=dev)
+        status = torch.empty(max_pairs, dtype=torch.int32, device=dev)
+        # each plaintext (at most its token's length - 48 bytes) is written inside its own token's span
+        device.decrypt(ks, un, tok_off, tok_len, pt, tok_off, pt_len, status, stream=stream)
     return {"pt": pt, "pt_off": tok_off, "pt_len": pt_len, "status": status, "ifac": ifac,
             "ifac_status": ifac_status, "fields": fields, "frame_pair": frame_pair, "n_frames": n_frames,
             "frame_status": d_st, "counts": counts}
@@ -124,12 +129,4 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
 
 def _on(stream):
     """torch plumbing on the pipeline's stream (the device calls take it explicitly)."""
-    return torch.cuda.stream(stream) if stream is not None else _null()
-
-
-class _null:
-    def __enter__(self):
-        return self
-
-    def __exit__(self, *a):
-        return False
+    return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()

@@ -88,3 +88,32 @@ def test_inbound_tampered_tag_fails_that_packet_alone():
     assert int(res["n_frames"]) == n
     assert sorted(np.nonzero(st)[0].tolist()) == hit and all(st[i] == 2 for i in hit)      # RT_BAD_HMAC
     assert bool((res["pt_len"][:n].cpu()[torch.from_numpy(st == 0)] == L).all())
+
+
+def test_pipeline_on_a_side_stream_matches_default_stream():
+    """Every stage, the torch plumbing between them included, runs on the
+    stream it is given: the same batch through a side stream gives the same
+    stream bytes and plaintexts as through the current stream."""
+    import torch
+    import reticulum_amd as rt
+    from reticulum_amd import pipeline
+    n, L, isz = 600, 383, 16
+    key, ifac_key, pt, iv, dh, ctx, ifac, t = _case(n, L, isz, 5)
+    ks = rt.KeySet(key, device=0)
+    args = (t(pt), t(iv), t(dh), t(ctx), t(ifac), t(np.frombuffer(ifac_key, np.uint8)))
+    framed0, foff0 = pipeline.outbound(ks, *args)
+    total = int(foff0[-1])
+    ref0 = pipeline.inbound(ks, framed0[:total].clone(), args[5], isz, 2 * n)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    framed1, foff1 = pipeline.outbound(ks, *args, stream=s)
+    res1 = pipeline.inbound(ks, framed1[:total], args[5], isz, 2 * n, stream=s)
+    s.synchronize()
+    assert torch.equal(framed1[:total], framed0[:total]) and torch.equal(foff1, foff0)
+    for k in ("status", "pt_len", "pt_off", "frame_pair"):
+        assert torch.equal(res1[k], ref0[k]), k
+    assert torch.equal(res1["ifac"][:n], ref0["ifac"][:n])      # entries past the frames are not written
+    po = ref0["pt_off"][:n].cpu().numpy()
+    p0, p1 = ref0["pt"].cpu().numpy(), res1["pt"].cpu().numpy()
+    assert all((p0[o:o + L] == p1[o:o + L]).all() for o in po)

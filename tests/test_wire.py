@@ -279,8 +279,9 @@ def test_gpu_device_forms_match_host_forms():
 @pytest.mark.gpu
 @pytest.mark.parametrize("density", [0.0, 0.02, 0.3, 0.9])
 def test_gpu_deframe_escape_dense_writes_only_frames(density):
-    """Unescape's row-wide 16-B stores (a lane stores its kept bytes and then
-    its neighbour's first ones, which the neighbour stores too): frames of
+    """Framing's and unescape's row-wide 16-B stores (a lane stores its own
+    bytes and then its neighbour's first ones, which the neighbour stores
+    too): the framed stream equals the oracle's, and frames of
     0-700 B whose bytes are 7E/7D with the given probability (lanes with many
     escapes keep as few as 8 of their 16 bytes) come back exact, and no byte of
     the output buffer outside the frames' own output is written."""
@@ -294,6 +295,8 @@ def test_gpu_deframe_escape_dense_writes_only_frames(density):
         a[hit] = rng.choice(np.array([0x7E, 0x7D], np.uint8), int(hit.sum()))
         pk.append(a.tobytes())
     stream, _ = wire.hdlc_frame_batch(pk)
+    # the framing side of the same row-wide stores: the stream is the reference's escape of every packet
+    assert stream == b"".join(ow.hdlc_frame(p) for p in pk)
     dev = torch.device("cuda", 0)
     buf = torch.from_numpy(np.frombuffer(stream, np.uint8).copy()).to(dev)
     total = len(stream)

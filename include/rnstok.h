@@ -351,6 +351,11 @@ int rt_packet_pack_headers(rt_ctx *ctx, const uint8_t *flags, const uint8_t *hop
                            const uint64_t *out_off, uint32_t n, void *stream);
 
 /* ---- memory helpers (so a non-torch host can drive the device API) ------- */
+/* rt_memcpy_d2h: a pinned (page-locked, mapped) destination, e.g. from
+ * rt_host_alloc, is written by GPU stores into the mapped buffer on `stream`
+ * (faster than the copy engine's device-to-host path on MI355X, and it
+ * shares the link with a copy-engine H2D); a pageable one is copied with
+ * hipMemcpyAsync.  Either way `dst` is valid once `stream` has run. */
 void *rt_device_alloc(rt_ctx *ctx, uint64_t bytes);
 void  rt_device_free(rt_ctx *ctx, void *p);
 void *rt_host_alloc(uint64_t bytes);            /* pinned */

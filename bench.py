@@ -361,12 +361,16 @@ def main():
     # once on its own shard, over its own PCIe link (the node's host-origin rate)
     # (N > 1: below, after the headline line exists, under a deadline)
     e2e = e2e_rate(ks, pt, iv, L, tl, n, stream) if args.e2e and world == 1 else None
-    node = None
+    node = shard8 = None
     if args.node and world == 1 and args.config == "c2":
         try:
             node = node_rate(dev)
         except Exception as exc:          # never fatal for the headline
             node = {"error": f"{type(exc).__name__}: {exc}"}
+        try:
+            shard8 = shard_rate(dev, _native.load().rt_num_cus(_native.context(local)))
+        except Exception as exc:
+            shard8 = {"error": f"{type(exc).__name__}: {exc}"}
 
     lib = _native.load()
     n_cu = lib.rt_num_cus(_native.context(local))
@@ -464,6 +468,7 @@ def main():
         "other_layout": other,
         "e2e_pcie": e2e,
         "node_pipeline": node,
+        "c4_rank_share_8gpu": shard8,
         "sharded_c4": None,
     }
 
@@ -1032,6 +1037,55 @@ def node_rate(dev, steps=10, g=None, n=1 << 20, L=383, isz=16):
     res["note"] = ("reticulum_amd.pipeline: outbound = token encrypt, Packet.pack header, IFAC mask, HDLC framing "
                    "(one stream); inbound = HDLC deframing, IFAC unmask, Packet.unpack + hash, token decrypt; "
                    "device-resident, one link key, synthetic payloads; DESIGN.md \u00a74.8")
+    return res
+
+
+def shard_rate(dev, n_cu, steps=10, L=16384, per_cu=128):
+    """The per-rank shape of c4 at 8 GPUs (32 768 x 16 KiB, 128
+    tokens per CU), device-resident on this GPU: the lane-cooperative long-token
+    kernels it routes to (k_encrypt_long4, k_decrypt_long2).
+    Median of ``steps`` HIP-event timings per direction after the clock
+    warmup, every token round-tripped, and the fraction of the integer-VALU
+    peak (the same canonical op count as the headline)."""
+    import torch
+    import reticulum_amd as rt
+    from reticulum_amd import _native, device
+    n = per_cu * n_cu
+    tl = rt.token_len(L)
+    g = torch.Generator(device=dev).manual_seed(4)
+    pt = torch.randint(0, 256, (n, L), dtype=torch.uint8, device=dev, generator=g)
+    iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
+    tok = torch.empty((n, tl), dtype=torch.uint8, device=dev)
+    back = torch.empty((n, tl - 48), dtype=torch.uint8, device=dev)
+    ol = torch.empty(n, dtype=torch.int32, device=dev)
+    st = torch.empty(n, dtype=torch.int32, device=dev)
+    ks = rt.KeySet(bytes(range(64)), device=dev.index if dev.index is not None else 0)
+    stream = torch.cuda.current_stream(dev)
+    enc = lambda: device.encrypt_uniform(ks, pt, L, iv, tok, stream=stream)
+    dec = lambda: device.decrypt_uniform(ks, tok, tl, back, ol, st, stream=stream)
+    enc()
+    dec()
+    torch.cuda.synchronize()
+    ok = bool((st == 0).all()) and torch.equal(back[:, :L], pt)
+    lib = _native.load()
+    ctx = _native.context(dev.index if dev.index is not None else 0)
+    res = {"tokens": n, "token_plaintext_bytes": L, "tokens_per_cu": per_cu, "ok": ok,
+           "kernels": {"encrypt": int(lib.rt_plan_uniform(ctx, n, L, 0, 0)),
+                       "decrypt": int(lib.rt_plan_uniform(ctx, n, tl, 0, 1))}}
+    peak = n_cu * 128 * 2.4e9
+    for name, f, ops in (("encrypt", enc, ops_enc(L)), ("decrypt", dec, ops_dec(L))):
+        warmup(f, stream, 2, 0.3)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for a, b in ev:
+            a.record(stream)
+            f()
+            b.record(stream)
+        torch.cuda.synchronize()
+        ms = sorted(a.elapsed_time(b) for a, b in ev)[steps // 2]
+        res[name] = {"ms": ms, "tokens_s": n / (ms * 1e-3), "frac_of_valu_peak": ops * n / (ms * 1e-3) / peak}
+    res["note"] = ("one rank's share of c4 at 8 GPUs; CBC encryption is a serial chain per token, so this shape "
+                   "is bound by the chain's round latency, not by issue (DESIGN.md \u00a74.2); kernels = "
+                   "RT_KERNEL_* from rt_plan_uniform")
     return res
 
 

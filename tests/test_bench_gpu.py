@@ -44,3 +44,13 @@ def test_node_rate_small():
     r = bench.node_rate(torch.device("cuda", 0), steps=3, n=4096)
     assert r["ok"] is True and r["packets"] == 4096
     assert r["outbound"]["ms"] > 0 and r["inbound"]["ms"] > 0 and r["stream_bytes"] > 4096 * 467
+
+
+def test_shard_rate_small():
+    """bench.shard_rate (the c4 8-GPU per-rank shape in the bench line) at a
+    small per-CU count: long-token kernels, every token back."""
+    import torch
+    import bench
+    r = bench.shard_rate(torch.device("cuda", 0), 8, steps=3, L=4096, per_cu=16)
+    assert r["ok"] is True and r["tokens"] == 128
+    assert r["encrypt"]["ms"] > 0 and r["decrypt"]["ms"] > 0 and 0 < r["encrypt"]["frac_of_valu_peak"] < 1

@@ -24,6 +24,9 @@
  *   rt_ifac_unmask     IFAC on inbound           RNS/Transport.py:1441-1475
  *   rt_packet_unpack   Packet.unpack + get_hash  RNS/Packet.py:236-268, 342-353
  *   rt_packet_pack_headers  Packet.pack header   RNS/Packet.py:167-228
+ *   rt_frames_compact  frames a read hands on    RNS/Interfaces/TCPInterface.py:391-401
+ *                      (one process_incoming call per frame, in stream order)
+ *   rt_token_spans     packet.data (the token)   RNS/Packet.py:262-275 (data after the header)
  *   rt_keyset_create_hkdf  per-packet keying     Identity.py:837-846 (hkdf -> Token(derived_key)),
  *                                                Link.py handshake key derivation
  *   rt_verify_trials*  ratchet trial loop        Identity.py:865-878 (first ratchet whose key
@@ -310,6 +313,17 @@ uint64_t rt_hdlc_deframe_workspace_bytes(uint64_t len);
 int rt_hdlc_deframe(rt_ctx *ctx, const uint8_t *buf, uint64_t len, uint32_t hw_mtu, uint32_t ifac_size, uint8_t *out,
                     uint64_t *frame_off, uint32_t *frame_len, int32_t *status, uint64_t *counts, uint64_t max_pairs,
                     void *workspace, void *stream);
+/* The frames one rt_hdlc_deframe pass hands on (pair k < counts[0] with
+ * status[k] == RT_FRAME_OK), in stream order, to the front of f_off / f_len
+ * (their offsets and lengths in the deframed buffer) and frame_pair (k);
+ * *n_frames (device int64) = their number.  Entries n_frames .. max_pairs-1
+ * are f_off 0, f_len 0, frame_pair -1, so per-packet stages can run over all
+ * max_pairs entries without the host learning n_frames.  DEVICE pointers;
+ * `workspace` of rt_frames_compact_workspace_bytes(max_pairs) bytes. */
+uint64_t rt_frames_compact_workspace_bytes(uint64_t max_pairs);
+int rt_frames_compact(rt_ctx *ctx, const uint64_t *frame_off, const uint32_t *frame_len, const int32_t *status,
+                      const uint64_t *counts, uint64_t max_pairs, uint64_t *f_off, uint32_t *f_len,
+                      int64_t *frame_pair, int64_t *n_frames, void *workspace, void *stream);
 /* IFAC on transmit: packet i (pkt + pkt_off[i], pkt_len[i] >= 2 bytes) with
  * its access code ifac + i*ifac_size (the last ifac_size bytes of the
  * interface identity's Ed25519 signature of the packet, computed by the
@@ -342,6 +356,13 @@ typedef struct rt_packet_fields {
 } rt_packet_fields;
 int rt_packet_unpack(rt_ctx *ctx, const uint8_t *pkt, const uint64_t *pkt_off, const uint32_t *pkt_len,
                      rt_packet_fields *fields, uint32_t n, void *stream);
+/* The token inside each unpacked packet: tok_off[i] = pkt_off[i] +
+ * fields[i].data_offset, tok_len[i] = fields[i].data_len where fields[i].ok;
+ * tok_off[i] = pkt_off[i], tok_len[i] = 0 (rejected by rt_decrypt as too
+ * short) elsewhere.  Feeds rt_decrypt straight from rt_packet_unpack's
+ * records.  DEVICE pointers. */
+int rt_token_spans(rt_ctx *ctx, const rt_packet_fields *fields, const uint64_t *pkt_off, uint32_t n,
+                   uint64_t *tok_off, uint32_t *tok_len, void *stream);
 /* Packet.pack's header for n packets at out + out_off[i]: flags, hops (NULL:
  * 0), [transport_id (16 B each; NULL: HEADER_1 for all)], destination hash
  * (16 B each), context — 19 or 35 bytes; the payload (a token from

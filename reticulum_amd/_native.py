@@ -59,6 +59,9 @@ SIGNATURES = [
     ("rt_ifac_mask", _int, [_vp, _vp, _vp, _vp, _vp, _u32, _vp, _u32, _vp, _vp, _u32, _vp]),
     ("rt_ifac_unmask", _int, [_vp, _vp, _vp, _vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp]),
     ("rt_packet_unpack", _int, [_vp, _vp, _vp, _vp, _vp, _u32, _vp]),
+    ("rt_frames_compact_workspace_bytes", _u64, [_u64]),
+    ("rt_frames_compact", _int, [_vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("rt_token_spans", _int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp]),
     ("rt_packet_pack_headers", _int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),
     ("rt_device_alloc", _vp, [_vp, _u64]),
     ("rt_device_free", None, [_vp, _vp]),

@@ -844,6 +844,22 @@ int rt_hdlc_deframe(rt_ctx *c, const uint8_t *buf, uint64_t len, uint32_t hw_mtu
     return RT_OK;
 }
 
+uint64_t rt_frames_compact_workspace_bytes(uint64_t max_pairs) { return frames_compact_workspace_bytes(max_pairs); }
+
+int rt_frames_compact(rt_ctx *c, const uint64_t *frame_off, const uint32_t *frame_len, const int32_t *status,
+                      const uint64_t *counts, uint64_t max_pairs, uint64_t *f_off, uint32_t *f_len,
+                      int64_t *frame_pair, int64_t *n_frames, void *workspace, void *stream) {
+    if (!c) return fail(RT_E_INVAL, "null context");
+    if (!counts || !n_frames) return fail(RT_E_INVAL, "rt_frames_compact: null counts/n_frames");
+    if (max_pairs && (!frame_off || !frame_len || !status || !f_off || !f_len || !frame_pair || !workspace))
+        return fail(RT_E_INVAL, "rt_frames_compact: null buffer");
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    RT_HIP(launch_frames_compact(frame_off, frame_len, status, counts, max_pairs, f_off, f_len, frame_pair, n_frames,
+                                 workspace, pick(c, stream)),
+           "frames compact");
+    return RT_OK;
+}
+
 int rt_ifac_mask(rt_ctx *c, const uint8_t *pkt, const uint64_t *pkt_off, const uint32_t *pkt_len, const uint8_t *ifac,
                  uint32_t ifac_size, const uint8_t *ifac_key, uint32_t key_len, uint8_t *out, const uint64_t *out_off,
                  uint32_t n, void *stream) {
@@ -882,6 +898,16 @@ int rt_packet_unpack(rt_ctx *c, const uint8_t *pkt, const uint64_t *pkt_off, con
     if (!pkt || !pkt_off || !pkt_len || !fields) return fail(RT_E_INVAL, "rt_packet_unpack: null buffer");
     RT_HIP(hipSetDevice(c->device), "hipSetDevice");
     RT_HIP(launch_unpack(pkt, pkt_off, pkt_len, fields, n, pick(c, stream)), "packet unpack");
+    return RT_OK;
+}
+
+int rt_token_spans(rt_ctx *c, const rt_packet_fields *fields, const uint64_t *pkt_off, uint32_t n, uint64_t *tok_off,
+                   uint32_t *tok_len, void *stream) {
+    if (!c) return fail(RT_E_INVAL, "null context");
+    if (n == 0) return RT_OK;
+    if (!fields || !pkt_off || !tok_off || !tok_len) return fail(RT_E_INVAL, "rt_token_spans: null buffer");
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    RT_HIP(launch_token_spans(fields, pkt_off, n, tok_off, tok_len, pick(c, stream)), "token spans");
     return RT_OK;
 }
 

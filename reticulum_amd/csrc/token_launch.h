@@ -126,6 +126,12 @@ hipError_t launch_hdlc_deframe(const uint8_t *buf, uint64_t len, uint32_t hw_mtu
                                uint64_t *frame_off, uint32_t *frame_len, int32_t *status, uint64_t *counts,
                                uint64_t max_pairs, void *ws, hipStream_t s);
 hipError_t launch_ifac(const IfacArgs &a, bool mask, hipStream_t s);
+uint64_t frames_compact_workspace_bytes(uint64_t max_pairs);
+hipError_t launch_frames_compact(const uint64_t *d_off, const uint32_t *d_len, const int32_t *st,
+                                 const uint64_t *counts, uint64_t max_pairs, uint64_t *f_off, uint32_t *f_len,
+                                 int64_t *frame_pair, int64_t *n_frames, void *ws, hipStream_t s);
+hipError_t launch_token_spans(const void *fields, const uint64_t *pkt_off, uint32_t n, uint64_t *tok_off,
+                              uint32_t *tok_len, hipStream_t s);
 hipError_t launch_unpack(const uint8_t *pkt, const uint64_t *off, const uint32_t *len, void *fields, uint32_t n,
                          hipStream_t s);
 hipError_t launch_pack_headers(const PackArgs &a, hipStream_t s);

@@ -20,6 +20,8 @@
 //   k_ifac           mask (outbound) / unmask (inbound) with HKDF(ifac, ifac_key)
 //   k_unpack         header fields + SHA-256 packet hash
 //   k_pack_headers   flags, hops, [transport id], destination hash, context
+//   k_compact_*      the frames the read loop hands on, to the front in order
+//   k_token_spans    each unpacked packet's data span (the token)
 #include "token_device.h"
 #include "token_launch.h"
 #include "../../include/rnstok.h"
@@ -740,6 +742,66 @@ __global__ __launch_bounds__(256) void k_ifac(IfacArgs a) {
     }
 }
 
+// ------------------------------------------------------ frame compaction --
+//
+// The frames a read hands to Transport (TCPInterface.py:391-401: pair k <
+// counts[0] with status RT_FRAME_OK), in stream order, at the front of the
+// per-frame arrays; one pair per thread, SCAN_BLOCK per workgroup.  Pass 1
+// counts each block's frames, k_scan_parts places the blocks, pass 2 writes
+// the frames and clears the entries past the last one.
+__device__ __forceinline__ bool handed_on(const int32_t *st, uint64_t pairs, uint64_t k) {
+    return k < pairs && st[k] == RT_FRAME_OK;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_compact_count(const int32_t *st, const uint64_t *counts, uint64_t n,
+                                                              uint64_t *part) {
+    const uint64_t k = (uint64_t)blockIdx.x * SCAN_BLOCK + threadIdx.x;
+    const int c = __syncthreads_count(handed_on(st, min(counts[0], n), k));
+    if (threadIdx.x == 0) part[blockIdx.x] = (uint64_t)c;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_compact_write(const uint64_t *d_off, const uint32_t *d_len,
+                                                              const int32_t *st, const uint64_t *counts, uint64_t n,
+                                                              const uint64_t *part, uint64_t nb, uint64_t *f_off,
+                                                              uint32_t *f_len, int64_t *frame_pair,
+                                                              int64_t *n_frames) {
+    __shared__ uint32_t wave_n[SCAN_BLOCK / 64];
+    const uint64_t k = (uint64_t)blockIdx.x * SCAN_BLOCK + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const bool ok = handed_on(st, min(counts[0], n), k);
+    const uint64_t bal = __ballot(ok);
+    if (lane == 0) wave_n[w] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t before = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+    for (uint32_t j = 0; j < w; ++j) before += wave_n[j];
+    const uint64_t total = part[nb];
+    if (ok) {
+        const uint64_t r = part[blockIdx.x] + before;
+        f_off[r] = d_off[k];
+        f_len[r] = d_len[k];
+        frame_pair[r] = (int64_t)k;
+    }
+    if (k < n && k >= total) {          // past the frames: empty, rejected by every later stage
+        f_off[k] = 0;
+        f_len[k] = 0;
+        frame_pair[k] = -1;
+    }
+    if (k == 0) *n_frames = (int64_t)total;
+}
+
+// Packet.unpack's data (Packet.py:262-275): the token of packet i is
+// pkt[pkt_off[i] + data_offset, + data_len) where unpack succeeded; an empty
+// span at pkt_off[i] elsewhere (rejected by the decrypt as too short).
+__global__ __launch_bounds__(256) void k_token_spans(const rt_packet_fields *f, const uint64_t *pkt_off, uint32_t n,
+                                                     uint64_t *tok_off, uint32_t *tok_len) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t *r = (const uint32_t *)(f + i);       // ok in byte 0, data_offset / data_len in words 3 / 4
+    const bool ok = (r[0] & 0xFFu) == 1u;
+    tok_off[i] = pkt_off[i] + (ok ? r[3] : 0u);
+    tok_len[i] = ok ? r[4] : 0u;
+}
+
 // --------------------------------------------------------- packet header --
 
 // SHA-256 over  first || src[0..len): the full 64-B blocks from 16-B loads
@@ -942,6 +1004,29 @@ hipError_t launch_unpack(const uint8_t *pkt, const uint64_t *off, const uint32_t
                          hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_unpack, dim3((n + 255) / 256), dim3(256), 0, s, pkt, off, len, (rt_packet_fields *)fields, n);
+    return hipGetLastError();
+}
+
+uint64_t frames_compact_workspace_bytes(uint64_t max_pairs) { return scan_workspace_bytes(max_pairs); }
+
+hipError_t launch_frames_compact(const uint64_t *d_off, const uint32_t *d_len, const int32_t *st,
+                                 const uint64_t *counts, uint64_t max_pairs, uint64_t *f_off, uint32_t *f_len,
+                                 int64_t *frame_pair, int64_t *n_frames, void *ws, hipStream_t s) {
+    if (max_pairs == 0) return hipMemsetAsync(n_frames, 0, 8, s);
+    const uint64_t nb = (max_pairs + SCAN_BLOCK - 1) / SCAN_BLOCK;
+    uint64_t *part = (uint64_t *)ws;
+    hipLaunchKernelGGL(k_compact_count, dim3((unsigned)nb), dim3(SCAN_BLOCK), 0, s, st, counts, max_pairs, part);
+    hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(SCAN_BLOCK), 0, s, part, nb);
+    hipLaunchKernelGGL(k_compact_write, dim3((unsigned)nb), dim3(SCAN_BLOCK), 0, s, d_off, d_len, st, counts,
+                       max_pairs, part, nb, f_off, f_len, frame_pair, n_frames);
+    return hipGetLastError();
+}
+
+hipError_t launch_token_spans(const void *fields, const uint64_t *pkt_off, uint32_t n, uint64_t *tok_off,
+                              uint32_t *tok_len, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_token_spans, dim3((n + 255) / 256), dim3(256), 0, s, (const rt_packet_fields *)fields,
+                       pkt_off, n, tok_off, tok_len);
     return hipGetLastError();
 }
 

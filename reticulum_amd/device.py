@@ -387,6 +387,45 @@ def hdlc_deframe(buf, out, frame_off, frame_len, status, counts, hw_mtu=262144, 
                                       _p(frame_len), _p(status), _p(counts), max_pairs, _p(ws), _stream(stream, buf.device)))
 
 
+def frames_compact(frame_off, frame_len, status, counts, f_off, f_len, frame_pair, n_frames, workspace=None,
+                   stream=None):
+    """The frames an hdlc_deframe pass hands on (pair k < counts[0] with
+    status RT_FRAME_OK; TCPInterface.py:391-401), in stream order, to the
+    front of f_off (int64) / f_len (int32) / frame_pair (int64, the pair
+    index); n_frames (a 0-d int64 device tensor) gets their number, and the
+    entries past it are f_off 0, f_len 0, frame_pair -1.  All arrays have
+    max_pairs = frame_off.numel() entries."""
+    max_pairs = frame_off.numel()
+    if any(t.numel() != max_pairs for t in (frame_len, status, f_off, f_len, frame_pair)) or \
+            counts.numel() < 2 or n_frames.numel() != 1:
+        raise ValueError("shape mismatch")
+    if frame_off.dtype != torch.int64 or f_off.dtype != torch.int64 or frame_pair.dtype != torch.int64 or \
+            n_frames.dtype != torch.int64 or frame_len.dtype != torch.int32 or f_len.dtype != torch.int32 or \
+            status.dtype != torch.int32 or counts.dtype != torch.int64:
+        raise TypeError("frames_compact: int64 offsets/pairs/counts, int32 lengths/status")
+    lib = _native.load()
+    ws = workspace if workspace is not None else torch.empty(
+        max(1, int(lib.rt_frames_compact_workspace_bytes(max_pairs))), dtype=torch.uint8, device=frame_off.device)
+    _native.check(lib.rt_frames_compact(_ctx_of(frame_off), _p(frame_off), _p(frame_len), _p(status), _p(counts),
+                                        max_pairs, _p(f_off), _p(f_len), _p(frame_pair), _p(n_frames), _p(ws),
+                                        _stream(stream, frame_off.device)))
+
+
+def token_spans(fields, pkt_off, tok_off, tok_len, stream=None):
+    """Packet.unpack's data (Packet.py:262-275), the token of each packet:
+    tok_off[i] = pkt_off[i] + data_offset, tok_len[i] = data_len where
+    fields[i] (an rt_packet_fields record from packet_unpack) is ok, else
+    pkt_off[i] and 0.  int64 offsets, int32 lengths."""
+    n = pkt_off.numel()
+    if fields.numel() != 96 * n or tok_off.numel() != n or tok_len.numel() != n:
+        raise ValueError("shape mismatch")
+    if pkt_off.dtype != torch.int64 or tok_off.dtype != torch.int64 or tok_len.dtype != torch.int32:
+        raise TypeError("token_spans: int64 offsets, int32 lengths")
+    lib = _native.load()
+    _native.check(lib.rt_token_spans(_ctx_of(fields), _p(fields), _p(pkt_off), n, _p(tok_off), _p(tok_len),
+                                     _stream(stream, fields.device)))
+
+
 def ifac_mask(pkt, pkt_off, pkt_len, ifac, ifac_key, out, out_off, stream=None):
     """Transport.transmit's IFAC step (Transport.py:1069-1101): packet i plus
     its access code ifac[i] (n, ifac_size) -> pkt_len[i] + ifac_size masked

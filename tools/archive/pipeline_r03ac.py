@@ -15,8 +15,8 @@ Inbound, as the interface's read loop hands frames to Transport:
     Packet.unpack + hash     Packet.py:242-275, 342-353
     Token.decrypt            Token.py:100-114 (Link/Identity.decrypt)
 
-Every stage is one of reticulum_amd.device's kernels, the rearranging of
-offsets and lengths between them included (frames_compact, token_spans), and
+Every stage is one of reticulum_amd.device's kernels; between them only
+offsets and lengths are rearranged (torch plumbing on the same stream), and
 nothing is synchronised: sizes the host does not know (the number of frames
 in a stream) stay on the device, and entries past them carry length 0, which
 every later stage rejects like the reference does (a frame too short for its
@@ -91,17 +91,21 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
     with _on(stream):      # temporaries allocated on the stream that uses them
         dev = buf.device
         out = torch.empty(buf.numel(), dtype=torch.uint8, device=dev)
-        d_off = torch.empty(max_pairs, dtype=torch.int64, device=dev)
-        d_len = torch.empty(max_pairs, dtype=torch.int32, device=dev)
+        d_off = torch.zeros(max_pairs, dtype=torch.int64, device=dev)
+        d_len = torch.zeros(max_pairs, dtype=torch.int32, device=dev)
         d_st = torch.full((max_pairs,), -1, dtype=torch.int32, device=dev)
         counts = torch.empty(2, dtype=torch.int64, device=dev)
         device.hdlc_deframe(buf, out, d_off, d_len, d_st, counts, hw_mtu=hw_mtu, ifac_size=ifac_size, stream=stream)
-        # the frames handed on, to the front in stream order; empty entries past them
-        f_off = torch.empty(max_pairs, dtype=torch.int64, device=dev)
-        f_len = torch.empty(max_pairs, dtype=torch.int32, device=dev)
-        frame_pair = torch.empty(max_pairs, dtype=torch.int64, device=dev)
-        n_frames = torch.empty((), dtype=torch.int64, device=dev)
-        device.frames_compact(d_off, d_len, d_st, counts, f_off, f_len, frame_pair, n_frames, stream=stream)
+        ok = (torch.arange(max_pairs, device=dev) < counts[0]) & (d_st == FRAME_OK)
+        rank = torch.cumsum(ok, 0, dtype=torch.int64) - 1
+        n_frames = rank[-1] + 1 if max_pairs else torch.zeros((), dtype=torch.int64, device=dev)
+        # scatter the OK frames to the front; everything else lands in a dump slot past the end
+        idx = torch.where(ok, rank, torch.full_like(rank, max_pairs))
+        f_off = torch.zeros(max_pairs + 1, dtype=torch.int64, device=dev).scatter_(0, idx, d_off)[:max_pairs]
+        f_len = torch.zeros(max_pairs + 1, dtype=torch.int32, device=dev).scatter_(0, idx, d_len)[:max_pairs]
+        frame_pair = torch.full((max_pairs + 1,), -1, dtype=torch.int64, device=dev).scatter_(
+            0, idx, torch.arange(max_pairs, device=dev))[:max_pairs]
+        f_off, f_len = f_off.contiguous(), f_len.contiguous()
         un = torch.empty_like(out)
         ifac = torch.empty((max_pairs, ifac_size), dtype=torch.uint8, device=dev)
         ifac_status = torch.empty(max_pairs, dtype=torch.int32, device=dev)
@@ -109,9 +113,10 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
         p_len = torch.where(ifac_status == 0, f_len - ifac_size, torch.zeros_like(f_len)).contiguous()
         fields = torch.empty((max_pairs, 96), dtype=torch.uint8, device=dev)
         device.packet_unpack(un, f_off, p_len, fields, stream=stream)
-        tok_off = torch.empty(max_pairs, dtype=torch.int64, device=dev)
-        tok_len = torch.empty(max_pairs, dtype=torch.int32, device=dev)
-        device.token_spans(fields, f_off, tok_off, tok_len, stream=stream)
+        words = fields.view(torch.int32)          # rt_packet_fields: data_offset, data_len at bytes 12..19
+        data_ok = fields[:, 0] == 1
+        tok_off = torch.where(data_ok, f_off + words[:, 3].to(torch.int64), f_off).contiguous()
+        tok_len = torch.where(data_ok, words[:, 4], torch.zeros_like(words[:, 4])).contiguous()
         pt = torch.empty_like(un)
         pt_len = torch.empty(max_pairs, dtype=torch.int32, device=dev)
         status = torch.empty(max_pairs, dtype=torch.int32, device=dev)

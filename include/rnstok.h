@@ -338,11 +338,13 @@ int rt_ifac_mask(rt_ctx *ctx, const uint8_t *pkt, const uint64_t *pkt_off, const
  * is longer than 2 + ifac_size; then its IFAC goes to ifac_out + i*ifac_size
  * and the unmasked packet without it (pkt_len[i] - ifac_size bytes, flag
  * cleared) to out + out_off[i].  status 1: the reference drops the packet
- * before signing.  The caller then compares ifac with the tail of
+ * before signing.  out_len (may be NULL) receives the unmasked length,
+ * pkt_len[i] - ifac_size, where status[i] is 0 and 0 elsewhere, ready as
+ * rt_packet_unpack's pkt_len.  The caller then compares ifac with the tail of
  * sign(unmasked packet) (Transport.py:1477-1481). */
 int rt_ifac_unmask(rt_ctx *ctx, const uint8_t *pkt, const uint64_t *pkt_off, const uint32_t *pkt_len,
                    uint32_t ifac_size, const uint8_t *ifac_key, uint32_t key_len, uint8_t *ifac_out, uint8_t *out,
-                   const uint64_t *out_off, int32_t *status, uint32_t n, void *stream);
+                   const uint64_t *out_off, int32_t *status, uint32_t *out_len, uint32_t n, void *stream);
 /* Packet.unpack + get_hash per packet (96 bytes).  ok = 0 where unpack
  * returns False (hop count >= 128, packet too short for its header). */
 typedef struct rt_packet_fields {

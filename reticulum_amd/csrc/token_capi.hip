@@ -870,7 +870,7 @@ int rt_ifac_mask(rt_ctx *c, const uint8_t *pkt, const uint64_t *pkt_off, const u
     if (!pkt || !pkt_off || !pkt_len || !ifac || !out || !out_off || (key_len && !ifac_key))
         return fail(RT_E_INVAL, "rt_ifac_mask: null buffer");
     IfacArgs a{pkt, pkt_off, pkt_len, const_cast<uint8_t *>(ifac), ifac_size, ifac_key, key_len, out, out_off,
-               nullptr, n};
+               nullptr, nullptr, n};
     RT_HIP(hipSetDevice(c->device), "hipSetDevice");
     RT_HIP(launch_ifac(a, true, pick(c, stream)), "ifac mask");
     return RT_OK;
@@ -878,14 +878,14 @@ int rt_ifac_mask(rt_ctx *c, const uint8_t *pkt, const uint64_t *pkt_off, const u
 
 int rt_ifac_unmask(rt_ctx *c, const uint8_t *pkt, const uint64_t *pkt_off, const uint32_t *pkt_len, uint32_t ifac_size,
                    const uint8_t *ifac_key, uint32_t key_len, uint8_t *ifac_out, uint8_t *out, const uint64_t *out_off,
-                   int32_t *status, uint32_t n, void *stream) {
+                   int32_t *status, uint32_t *out_len, uint32_t n, void *stream) {
     if (!c) return fail(RT_E_INVAL, "null context");
     if (key_len > 64) return fail(RT_E_INVAL, "rt_ifac_unmask: ifac_key longer than 64 bytes");
     if (ifac_size == 0 || ifac_size > 64) return fail(RT_E_INVAL, "rt_ifac_unmask: ifac_size must be 1..64");
     if (n == 0) return RT_OK;
     if (!pkt || !pkt_off || !pkt_len || !ifac_out || !out || !out_off || !status || (key_len && !ifac_key))
         return fail(RT_E_INVAL, "rt_ifac_unmask: null buffer");
-    IfacArgs a{pkt, pkt_off, pkt_len, ifac_out, ifac_size, ifac_key, key_len, out, out_off, status, n};
+    IfacArgs a{pkt, pkt_off, pkt_len, ifac_out, ifac_size, ifac_key, key_len, out, out_off, status, out_len, n};
     RT_HIP(hipSetDevice(c->device), "hipSetDevice");
     RT_HIP(launch_ifac(a, false, pick(c, stream)), "ifac unmask");
     return RT_OK;

@@ -108,6 +108,7 @@ struct IfacArgs {
     uint8_t *out;
     const uint64_t *out_off;
     int32_t *status;               // unmask only
+    uint32_t *out_len;             // unmask only, may be null: unmasked length (0 where status != 0)
     uint32_t n;
 };
 struct PackArgs {

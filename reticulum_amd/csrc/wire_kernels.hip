@@ -646,6 +646,7 @@ __global__ __launch_bounds__(256) void k_ifac(IfacArgs a) {
         // len(raw) > 2, IFAC flag set, len(raw) > 2 + ifac_size (:1441-1445)
         const bool ok = L > 2u && (raw[0] & 0x80u) && L > 2u + n;
         a.status[i] = ok ? 0 : 1;
+        if (a.out_len) a.out_len[i] = ok ? L - n : 0u;
         if (!ok) return;
         ifac = raw + 2;
         for (uint32_t k = 0; k < n; ++k) a.ifac[(uint64_t)i * n + k] = ifac[k];

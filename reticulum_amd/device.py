@@ -439,19 +439,22 @@ def ifac_mask(pkt, pkt_off, pkt_len, ifac, ifac_key, out, out_off, stream=None):
                                    _p(ifac_key), ifac_key.numel(), _p(out), _p(out_off), n, _stream(stream, pkt.device)))
 
 
-def ifac_unmask(pkt, pkt_off, pkt_len, ifac_key, ifac_out, out, out_off, status, stream=None):
+def ifac_unmask(pkt, pkt_off, pkt_len, ifac_key, ifac_out, out, out_off, status, out_len=None, stream=None):
     """Transport.inbound's IFAC step up to the signature check
     (Transport.py:1441-1475): status[i] = 0 with the IFAC in ifac_out[i] (n,
     ifac_size) and the unmasked packet (pkt_len[i] - ifac_size bytes) at
-    out[out_off[i]:], or 1 where the reference drops the packet first."""
+    out[out_off[i]:], or 1 where the reference drops the packet first.
+    out_len (n,) int32, if given, receives pkt_len[i] - ifac_size where the
+    status is 0 and 0 elsewhere (packet_unpack's lengths)."""
     _check_u8(pkt, ifac_key, ifac_out, out)
     n = pkt_off.numel()
-    if pkt_len.numel() != n or ifac_out.shape[0] != n or out_off.numel() != n or status.numel() != n:
+    if pkt_len.numel() != n or ifac_out.shape[0] != n or out_off.numel() != n or status.numel() != n or \
+            (out_len is not None and (out_len.numel() != n or out_len.dtype != torch.int32)):
         raise ValueError("shape mismatch")
     lib = _native.load()
     _native.check(lib.rt_ifac_unmask(_ctx_of(pkt), _p(pkt), _p(pkt_off), _p(pkt_len), ifac_out.shape[1],
                                      _p(ifac_key), ifac_key.numel(), _p(ifac_out), _p(out), _p(out_off), _p(status),
-                                     n, _stream(stream, pkt.device)))
+                                     _p(out_len), n, _stream(stream, pkt.device)))
 
 
 def packet_unpack(pkt, pkt_off, pkt_len, fields, stream=None):

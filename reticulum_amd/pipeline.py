@@ -105,8 +105,8 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
         un = torch.empty_like(out)
         ifac = torch.empty((max_pairs, ifac_size), dtype=torch.uint8, device=dev)
         ifac_status = torch.empty(max_pairs, dtype=torch.int32, device=dev)
-        device.ifac_unmask(out, f_off, f_len, ifac_key, ifac, un, f_off, ifac_status, stream=stream)
-        p_len = torch.where(ifac_status == 0, f_len - ifac_size, torch.zeros_like(f_len)).contiguous()
+        p_len = torch.empty(max_pairs, dtype=torch.int32, device=dev)
+        device.ifac_unmask(out, f_off, f_len, ifac_key, ifac, un, f_off, ifac_status, out_len=p_len, stream=stream)
         fields = torch.empty((max_pairs, 96), dtype=torch.uint8, device=dev)
         device.packet_unpack(un, f_off, p_len, fields, stream=stream)
         tok_off = torch.empty(max_pairs, dtype=torch.int64, device=dev)

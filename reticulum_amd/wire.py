@@ -239,7 +239,7 @@ def ifac_unmask_batch(raws, ifac_size, ifac_key, device=None):
         p_ifac = d.alloc(n * ifac_size)
         p_st = d.alloc(4 * n)
         _native.check(d.lib.rt_ifac_unmask(d.ctx, d.up(buf), d.up(off), d.up(lens), ifac_size, d.up(key), len(key),
-                                           p_ifac, p_out, d.up(out_off), p_st, n, None))
+                                           p_ifac, p_out, d.up(out_off), p_st, None, n, None))
         st = d.down(p_st, np.zeros(n, np.int32))
         ifac = d.down(p_ifac, np.zeros(n * ifac_size, np.uint8)).tobytes()
         out = d.down(p_out, np.zeros(max(int(lens.sum()), 1), np.uint8)).tobytes()

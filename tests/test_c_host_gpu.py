@@ -1,0 +1,30 @@
+"""The C-ABI driven from C alone (tests/c_host/c_host_roundtrip.c): the token
+host and device entry points and the whole interface path composed from
+rt_* calls, checked against the C oracle inside the program."""
+import os
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BIN = os.path.join(HERE, "c_host", "c_host_roundtrip")
+
+
+def _build():
+    subprocess.run(["make", "-s", "-C", os.path.join(HERE, "c_host")], check=True, timeout=120)
+
+
+def test_c_host_program_builds_against_the_header():
+    """CPU: the program compiles with -Werror against include/rnstok.h and
+    links against librnstok.so (every symbol it calls is exported)."""
+    _build()
+    assert os.access(BIN, os.X_OK)
+
+
+@pytest.mark.gpu
+def test_c_host_roundtrip():
+    if not os.access(BIN, os.X_OK):
+        _build()
+    r = subprocess.run([BIN], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert r.stdout.startswith("c_host ok"), r.stdout

@@ -265,6 +265,15 @@ def test_gpu_device_forms_match_host_forms():
     uh = un.cpu().numpy().tobytes()
     assert (ust.cpu().numpy() == 0).all() and torch.equal(i_out, ti)
     assert [uh[int(a):int(a) + int(b)] for a, b in zip(m_off, lens)] == [bytes([p[0] & 0x7F]) + p[1:] for p in pk]
+    # out_len: the unmasked length where the IFAC checks pass, 0 where the
+    # packet is dropped (here: every third one cut to 2 + ifac_size bytes)
+    short = tm_len.clone()
+    short[::3] = 10
+    o_len = torch.full((n,), 7, dtype=torch.int32, device=dev)
+    device.ifac_unmask(masked, tm_off, short, key, i_out, un, tm_off, ust, out_len=o_len)
+    drop = np.arange(n) % 3 == 0
+    assert np.array_equal(ust.cpu().numpy(), drop.astype(np.int32))
+    assert np.array_equal(o_len.cpu().numpy(), np.where(drop, 0, lens).astype(np.int32))
     # unpack
     fields = torch.empty((n, 96), dtype=torch.uint8, device=dev)
     device.packet_unpack(flat, t_off, t_len, fields)

@@ -79,9 +79,10 @@ def parse():
                     help="N > 1: chunks per rank of the pipelined sharded pass (0 disables it)")
     ap.add_argument("--sharded-timeout", type=float, default=150.0,
                     help="N > 1: seconds allowed for the sharded c4 pass after the headline")
-    ap.add_argument("--layout", choices=["rows", "interleaved"], default="interleaved",
-                    help="HBM layout the headline is timed on: the unit-interleaved device layout "
-                         "(rt_encrypt_interleaved, coalesced) or packed rows (the reference's byte strings); "
+    ap.add_argument("--layout", choices=["rows", "interleaved"], default="rows",
+                    help="HBM layout the headline is timed on: packed rows (default: the reference's byte strings, "
+                         "the layout socket bytes arrive in) or the unit-interleaved device layout "
+                         "(rt_encrypt_interleaved, coalesced, for batches produced on the device in that layout); "
                          "the other layout is timed right after it")
     ap.add_argument("--one-layout", action="store_true", help="time only --layout")
     ap.add_argument("--e2e", action="store_true", default=True, help="also time the PCIe-inclusive path")
@@ -361,7 +362,7 @@ def main():
     # once on its own shard, over its own PCIe link (the node's host-origin rate)
     # (N > 1: below, after the headline line exists, under a deadline)
     e2e = e2e_rate(ks, pt, iv, L, tl, n, stream) if args.e2e and world == 1 else None
-    node = shard8 = None
+    node = shard8 = c5share = None
     if args.node and world == 1 and args.config == "c2":
         try:
             node = node_rate(dev)
@@ -371,6 +372,14 @@ def main():
             shard8 = shard_rate(dev, _native.load().rt_num_cus(_native.context(local)))
         except Exception as exc:
             shard8 = {"error": f"{type(exc).__name__}: {exc}"}
+        try:
+            node["host"] = node_host_rate(dev)
+        except Exception as exc:
+            node["host"] = {"error": f"{type(exc).__name__}: {exc}"}
+        try:
+            c5share = c5_share_rate(dev, _native.load().rt_num_cus(_native.context(local)))
+        except Exception as exc:
+            c5share = {"error": f"{type(exc).__name__}: {exc}"}
 
     lib = _native.load()
     n_cu = lib.rt_num_cus(_native.context(local))
@@ -469,6 +478,7 @@ def main():
         "e2e_pcie": e2e,
         "node_pipeline": node,
         "c4_rank_share_8gpu": shard8,
+        "c5_rank_share_8gpu": c5share,
         "sharded_c4": None,
     }
 
@@ -1040,6 +1050,119 @@ def node_rate(dev, steps=10, g=None, n=1 << 20, L=383, isz=16):
     return res
 
 
+def node_host_rate(dev, n=1 << 20, L=383, isz=16, slices=32, n_streams=3, reps=3):
+    """The composed interface path host-origin (north_star: "This path starts
+    and ends in host memory (Interface socket buffers)"; TCPInterface.py:
+    387-401 -> Link.py:1175-1182 inbound, Link.py:1161 -> TCPInterface.py:323
+    outbound), pinned host buffers at both ends, `slices` slices round-robin
+    on `n_streams` streams so one slice's H2D, another's kernels and a third's
+    D2H overlap:
+    * outbound: plaintexts, IVs, destination hashes, contexts and IFACs H2D ->
+      pipeline.outbound -> the slice's HDLC stream D2H as GPU stores, its
+      length read on the device (device.copy_to_host_upto: the host does not
+      know a framed slice's length before it runs);
+    * inbound: the framed stream H2D in slices cut at frame boundaries (each
+      slice one read of the interface) -> pipeline.inbound -> the plaintext
+      buffer and the per-packet offsets, lengths and statuses D2H as GPU
+      stores.
+    Best of ``reps`` passes; a sample of plaintexts and every status checked on
+    the host copies, and the host stream equal to the device-resident one."""
+    import torch
+    import reticulum_amd as rt
+    from reticulum_amd import device, pipeline
+    g = torch.Generator(device=dev).manual_seed(6)
+    pt = torch.randint(0, 256, (n, L), dtype=torch.uint8, device=dev, generator=g)
+    iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
+    dh = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
+    ctx = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev, generator=g)
+    ifac = torch.randint(0, 256, (n, isz), dtype=torch.uint8, device=dev, generator=g)
+    ikey = torch.randint(0, 256, (64,), dtype=torch.uint8, device=dev, generator=g)
+    ks = rt.KeySet(bytes(range(64)), device=dev.index if dev.index is not None else 0)
+    framed, foff = pipeline.outbound(ks, pt, iv, dh, ctx, ifac, ikey)
+    torch.cuda.synchronize()
+    fo = foff.cpu()
+    total = int(fo[-1])
+    ins_h = [x.cpu().pin_memory() for x in (pt, iv, dh, ctx, ifac)]
+    ins_d = [torch.empty_like(x) for x in (pt, iv, dh, ctx, ifac)]
+    ml = 19 + rt.token_len(L) + isz
+    step = -(-n // slices)
+    cuts = [(a, min(a + step, n)) for a in range(0, n, step)]
+    cap = [(b - a) * (2 * ml + 2) for a, b in cuts]
+    cap_off = [sum(cap[:k]) for k in range(len(cap))]
+    out_h = torch.empty(sum(cap), dtype=torch.uint8).pin_memory()
+    olen_h = torch.zeros(len(cuts), dtype=torch.int64).pin_memory()
+    side = [torch.cuda.Stream(device=dev) for _ in range(n_streams)]
+    stream_h = framed[:total].cpu().pin_memory()
+    stream_d = torch.empty(total, dtype=torch.uint8, device=dev)
+    pt_h = torch.empty(total, dtype=torch.uint8).pin_memory()
+    meta_h = torch.empty(3 * n, dtype=torch.int64).pin_memory()     # per slice: (pt_off, pt_len, status) rows
+    hold = []
+
+    def outbound_pass():
+        hold.clear()
+        for k, (a, b) in enumerate(cuts):
+            s = side[k % n_streams]
+            with torch.cuda.stream(s):
+                for hx, dx in zip(ins_h, ins_d):
+                    dx[a:b].copy_(hx[a:b], non_blocking=True)
+                fr, fo_ = pipeline.outbound(ks, *(dx[a:b] for dx in ins_d), ikey, stream=s)
+                device.copy_to_host_upto(out_h[cap_off[k]:cap_off[k] + cap[k]], fr, fo_[-1:], stream=s)
+                device.copy_to_host(olen_h[k:k + 1], fo_[-1:], stream=s)
+                hold.append((fr, fo_))      # keep the slices' buffers alive until the pass is synchronised
+
+    def inbound_pass():
+        hold.clear()
+        for k, (a, b) in enumerate(cuts):
+            s = side[k % n_streams]
+            lo, hi = int(fo[a]), int(fo[b])
+            with torch.cuda.stream(s):
+                stream_d[lo:hi].copy_(stream_h[lo:hi], non_blocking=True)
+                r = pipeline.inbound(ks, stream_d[lo:hi], ikey, isz, 2 * (b - a), stream=s)
+                device.copy_to_host(pt_h[lo:hi], r["pt"], stream=s)
+                m = torch.stack([r["pt_off"][:b - a], r["pt_len"][:b - a].to(torch.int64),
+                                 r["status"][:b - a].to(torch.int64)])
+                device.copy_to_host(_meta_slot(meta_h, a, b), m, stream=s)
+                hold.append((r, m))
+
+    res = {"packets": n, "plaintext_bytes": L, "ifac_size": isz, "stream_bytes": total, "slices": len(cuts),
+           "streams": n_streams}
+    for name, f in (("outbound", outbound_pass), ("inbound", inbound_pass)):
+        best = float("inf")
+        for _ in range(reps + 1):         # the first pass warms the allocator and the clocks
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            f()
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t0)
+        res[name] = {"ms": best * 1e3, "packets_s": n / best,
+                     "pcie_gb_s": ((n * (L + 16 + 16 + 1 + isz) + total) if name == "outbound" else 2 * total)
+                     / best / 1e9}
+    # checks on the host copies: every slice's stream equals the device-resident one, statuses, plaintexts
+    ok = True
+    for k, (a, b) in enumerate(cuts):
+        lo, hi = int(fo[a]), int(fo[b])
+        ok = ok and int(olen_h[k]) == hi - lo and torch.equal(out_h[cap_off[k]:cap_off[k] + hi - lo], stream_h[lo:hi])
+    meta = torch.cat([_meta_slot(meta_h, a, b) for a, b in cuts], dim=1)
+    ok = ok and bool((meta[2] == 0).all()) and bool((meta[1] == L).all())
+    pt_c = pt.cpu()
+    for k, (a, b) in enumerate(cuts):
+        lo = int(fo[a])
+        for i in (a, (a + b) // 2, b - 1):
+            o = lo + int(_meta_slot(meta_h, a, b)[0, i - a])
+            ok = ok and torch.equal(pt_h[o:o + L], pt_c[i])
+    res["ok"] = ok
+    res["note"] = ("host-origin composed interface path: pinned host buffers at both ends, H2D on the copy engine, "
+                   "D2H as GPU stores into the pinned buffers, slices round-robin on streams; outbound pcie_gb_s "
+                   "counts inputs + framed stream, inbound the stream both ways (plaintext buffer = stream size)")
+    return res
+
+
+def _meta_slot(meta_h, a, b):
+    """Host rows (pt_off, pt_len, status) of packets [a, b) in node_host_rate's
+    pinned metadata buffer (one contiguous (3, b - a) block per slice)."""
+    return meta_h.view(-1)[3 * a:3 * b].view(3, b - a)
+
+
 def shard_rate(dev, n_cu, steps=10, L=16384, per_cu=128):
     """The per-rank shape of c4 at 8 GPUs (32 768 x 16 KiB, 128
     tokens per CU), device-resident on this GPU: the lane-cooperative long-token
@@ -1086,6 +1209,105 @@ def shard_rate(dev, n_cu, steps=10, L=16384, per_cu=128):
     res["note"] = ("one rank's share of c4 at 8 GPUs; CBC encryption is a serial chain per token, so this shape "
                    "is bound by the chain's round latency, not by issue (DESIGN.md \u00a74.2); kernels = "
                    "RT_KERNEL_* from rt_plan_uniform")
+    return res
+
+
+def c5_share_rate(dev, n_cu, n=1 << 20, steps=10, n_keys=65536):
+    """The per-rank shape of c5 at 8 GPUs (8 M packets of
+    64-4096 B, 65 536 keys, 50/50 encrypt/decrypt; one rank's share is 2^20
+    packets), device-resident on this GPU through the product's packed entry
+    points with length bucketing (rt_encrypt_ex / rt_decrypt_ex,
+    RT_F_SORT_BY_LENGTH: the bucketing passes are inside the timed region).
+    The first half of the packets is encrypted, the second half's tokens
+    (made before timing) are decrypted.  Median of ``steps`` HIP-event timings
+    per direction after the clock warmup; canonical ops summed over the real
+    lengths (352 per AES block, 1464 per SHA-256 compression,
+    +8 per tag compare); every decrypt status and length checked, and a
+    sample of plaintexts and tokens against each other (round trip)."""
+    import torch
+    import reticulum_amd as rt
+    from reticulum_amd import device
+    g = torch.Generator(device=dev).manual_seed(5)
+    kg = torch.Generator().manual_seed(55)
+    lens = torch.randint(64, 4097, (n,), dtype=torch.int32, generator=kg)
+    keys = torch.randint(0, 256, (n_keys, 64), dtype=torch.uint8, generator=kg).numpy()
+    ks = rt.KeySet(keys, device=dev.index if dev.index is not None else 0)
+    kidx = torch.randint(0, n_keys, (n,), dtype=torch.int32, device=dev, generator=g)
+    h = n // 2
+    le, ld = lens[:h].to(dev), lens[h:].to(dev)
+
+    def offs(x):
+        o = torch.zeros(x.numel(), dtype=torch.int64, device=dev)
+        o[1:] = torch.cumsum(x[:-1].to(torch.int64), 0)
+        return o
+
+    tlen = lambda x: (16 + 16 * (x // 16 + 1) + 32).to(torch.int32)     # noqa: E731
+    # encrypt half: plaintexts -> tokens
+    pe = torch.randint(0, 256, (int(le.to(torch.int64).sum()),), dtype=torch.uint8, device=dev, generator=g)
+    oe, ive = offs(le), torch.randint(0, 256, (h, 16), dtype=torch.uint8, device=dev, generator=g)
+    te_len = tlen(le)
+    te_off = offs(te_len)
+    te = torch.empty(int(te_len.to(torch.int64).sum()), dtype=torch.uint8, device=dev)
+    # decrypt half: tokens made before timing
+    pd = torch.randint(0, 256, (int(ld.to(torch.int64).sum()),), dtype=torch.uint8, device=dev, generator=g)
+    od, ivd = offs(ld), torch.randint(0, 256, (n - h, 16), dtype=torch.uint8, device=dev, generator=g)
+    td_len = tlen(ld)
+    td_off = offs(td_len)
+    td = torch.empty(int(td_len.to(torch.int64).sum()), dtype=torch.uint8, device=dev)
+    device.encrypt(ks, pd, od, ld, ivd, td, td_off, key_idx=kidx[h:], sort=True)
+    back = torch.empty(int((td_len - 48).to(torch.int64).sum()), dtype=torch.uint8, device=dev)
+    boff = offs(td_len - 48)
+    ol = torch.empty(n - h, dtype=torch.int32, device=dev)
+    st = torch.empty(n - h, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    enc = lambda: device.encrypt(ks, pe, oe, le, ive, te, te_off, key_idx=kidx[:h], sort=True, stream=stream)  # noqa
+    dec = lambda: device.decrypt(ks, td, td_off, td_len, back, boff, ol, st, key_idx=kidx[h:], sort=True,  # noqa
+                                 stream=stream)
+    enc()
+    dec()
+    torch.cuda.synchronize()
+    ok = bool((st == 0).all()) and torch.equal(ol, ld)
+    # round trip of a sample of the encrypt half's tokens, and the decrypt half's plaintexts
+    chk = torch.empty(int((te_len - 48).to(torch.int64).sum()), dtype=torch.uint8, device=dev)
+    cl = torch.empty(h, dtype=torch.int32, device=dev)
+    cs = torch.empty(h, dtype=torch.int32, device=dev)
+    device.decrypt(ks, te, te_off, te_len, chk, offs(te_len - 48), cl, cs, key_idx=kidx[:h], sort=True)
+    torch.cuda.synchronize()
+    ok = ok and bool((cs == 0).all()) and torch.equal(cl, le)
+    co = offs(te_len - 48).cpu()
+    oe_c, od_c, bo_c = oe.cpu(), od.cpu(), boff.cpu()
+    for i in range(0, h, 4099):
+        a, b, L = int(co[i]), int(oe_c[i]), int(lens[i])
+        ok = ok and torch.equal(chk[a:a + L], pe[b:b + L])
+        a, b, L = int(bo_c[i]), int(od_c[i]), int(lens[h + i])
+        ok = ok and torch.equal(back[a:a + L], pd[b:b + L])
+    L64 = lens.to(torch.int64)
+    B = L64 // 16 + 1
+    H = (64 + 16 + 16 * B + 9 + 63) // 64
+    ops = AES_BLOCK_OPS * B + SHA_CMP_OPS * H
+    ops_e, ops_d = int(ops[:h].sum()), int(ops[h:].sum()) + TAG_CMP_OPS * (n - h)
+    peak = n_cu * 128 * 2.4e9
+    res = {"packets": n, "keys": n_keys, "encrypt_packets": h, "decrypt_packets": n - h,
+           "plaintext_bytes": int(L64.sum()), "mean_plaintext_bytes": float(L64.float().mean()), "ok": ok,
+           "layout": "packed rows (byte strings at prefix-sum offsets), length-bucketed on the device"}
+    for name, f, o, bytes_ in (("encrypt", enc, ops_e, int(L64[:h].sum())), ("decrypt", dec, ops_d, int(L64[h:].sum()))):
+        warmup(f, stream, 2, 0.3)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for a, b in ev:
+            a.record(stream)
+            f()
+            b.record(stream)
+        torch.cuda.synchronize()
+        ms = sorted(a.elapsed_time(b) for a, b in ev)[steps // 2]
+        res[name] = {"ms": ms, "packets_s": (h if name == "encrypt" else n - h) / (ms * 1e-3),
+                     "gib_s": bytes_ / (ms * 1e-3) / 2**30, "canonical_ops": o,
+                     "frac_of_valu_peak": o / (ms * 1e-3) / peak}
+    tot = res["encrypt"]["ms"] + res["decrypt"]["ms"]
+    res["packets_s"] = n / (tot * 1e-3)
+    res["frac_of_valu_peak"] = (ops_e + ops_d) / (tot * 1e-3) / peak
+    res["note"] = ("one rank's share of c5 at 8 GPUs; per direction the length-bucketing passes (histogram, scan, "
+                   "scatter) and the per-key kernel are timed together; frac = canonical ops summed over the real "
+                   "lengths / time / (CUs x 128 x 2.4 GHz)")
     return res
 
 

@@ -318,8 +318,10 @@ int rt_hdlc_deframe(rt_ctx *ctx, const uint8_t *buf, uint64_t len, uint32_t hw_m
  * (their offsets and lengths in the deframed buffer) and frame_pair (k);
  * *n_frames (device int64) = their number.  Entries n_frames .. max_pairs-1
  * are f_off 0, f_len 0, frame_pair -1, so per-packet stages can run over all
- * max_pairs entries without the host learning n_frames.  DEVICE pointers;
- * `workspace` of rt_frames_compact_workspace_bytes(max_pairs) bytes. */
+ * max_pairs entries without the host learning n_frames.  The outputs must not
+ * overlap frame_off / frame_len (compaction in place would race; RT_E_INVAL).
+ * DEVICE pointers; `workspace` of rt_frames_compact_workspace_bytes(max_pairs)
+ * bytes. */
 uint64_t rt_frames_compact_workspace_bytes(uint64_t max_pairs);
 int rt_frames_compact(rt_ctx *ctx, const uint64_t *frame_off, const uint32_t *frame_len, const int32_t *status,
                       const uint64_t *counts, uint64_t max_pairs, uint64_t *f_off, uint32_t *f_len,
@@ -385,6 +387,12 @@ void *rt_host_alloc(uint64_t bytes);            /* pinned */
 void  rt_host_free(void *p);
 int   rt_memcpy_h2d(rt_ctx *ctx, void *dst, const void *src, uint64_t bytes, void *stream);
 int   rt_memcpy_d2h(rt_ctx *ctx, void *dst, const void *src, uint64_t bytes, void *stream);
+/* rt_memcpy_d2h_upto: min(max_bytes, *d_bytes) bytes, the count read on the
+ * device at run time (d_bytes: a DEVICE uint64, e.g. frame_off[n] of
+ * rt_hdlc_frame, a size the host does not know without a sync), as GPU
+ * stores into a pinned `dst` (RT_E_INVAL for any other destination). */
+int   rt_memcpy_d2h_upto(rt_ctx *ctx, void *dst, const void *src, uint64_t max_bytes, const uint64_t *d_bytes,
+                         void *stream);
 int   rt_stream_sync(rt_ctx *ctx, void *stream);
 
 #ifdef __cplusplus

@@ -20,9 +20,16 @@ namespace {
 typedef unsigned int u32x4c __attribute__((ext_vector_type(4)));
 
 // dst + head is 16-B aligned; the body is `body` aligned 16-B stores, the
-// head and tail bytes are stored one by one by the first 32 threads.
+// head and tail bytes are stored one by one by the first 32 threads.  With
+// `dev_bytes` the byte count is min(bytes, *dev_bytes), read on the device
+// (a size the host does not know, e.g. the end offset of an HDLC stream).
 __global__ __launch_bounds__(256) void k_store_host(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
-                                                    uint64_t bytes, uint32_t head) {
+                                                    uint64_t bytes, uint32_t head, const uint64_t *dev_bytes) {
+    if (dev_bytes) {
+        const uint64_t d = *dev_bytes;
+        bytes = d < bytes ? d : bytes;
+        head = (uint32_t)(head < bytes ? head : bytes);
+    }
     const uint64_t body = (bytes - head) >> 4;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint8_t *s = src + head;
@@ -41,12 +48,13 @@ __global__ __launch_bounds__(256) void k_store_host(const uint8_t *__restrict__ 
 
 }  // namespace
 
-hipError_t launch_store_host(uint8_t *dst_dev, const uint8_t *src, uint64_t bytes, hipStream_t s) {
+hipError_t launch_store_host(uint8_t *dst_dev, const uint8_t *src, uint64_t bytes, hipStream_t s,
+                             const uint64_t *dev_bytes) {
     if (!bytes) return hipSuccess;
     const uint32_t head = (uint32_t)std::min<uint64_t>((16u - ((uintptr_t)dst_dev & 15u)) & 15u, bytes);
     const uint64_t body = (bytes - head) >> 4;
     const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((body + 255) / 256, 2048));
-    hipLaunchKernelGGL(k_store_host, dim3((unsigned)blocks), dim3(256), 0, s, src, dst_dev, bytes, head);
+    hipLaunchKernelGGL(k_store_host, dim3((unsigned)blocks), dim3(256), 0, s, src, dst_dev, bytes, head, dev_bytes);
     return hipGetLastError();
 }
 

@@ -204,13 +204,21 @@ static hipStream_t pick(const rt_ctx *, void *stream) { return (hipStream_t)stre
 // is written by GPU stores (launch_store_host: 54 GB/s, and it shares the
 // link with a copy-engine H2D at 87 GB/s in total, against 30 GB/s for the
 // copy engine's D2H, profiles/r03n_pcie_probe.json); a pageable one goes
-// through hipMemcpyAsync.
-static hipError_t copy_d2h(void *dst, const void *src, uint64_t bytes, hipStream_t s) {
+// through hipMemcpyAsync.  The store kernel runs on the stream's GPU, so it
+// is used only when src is device memory of that GPU (`device`); any other
+// source (host memory, another GPU's buffer) takes hipMemcpyAsync, which
+// handles every source the copy engine can read.
+static bool query(hipPointerAttribute_t *at, const void *p) {
+    if (hipPointerGetAttributes(at, p) == hipSuccess) return true;
+    (void)hipGetLastError();       // a pageable pointer is an "invalid value" to the query: clear only that
+    return false;
+}
+static hipError_t copy_d2h(void *dst, const void *src, uint64_t bytes, hipStream_t s, int device) {
     if (!bytes) return hipSuccess;
-    hipPointerAttribute_t at;
-    if (hipPointerGetAttributes(&at, dst) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer)
-        return launch_store_host((uint8_t *)at.devicePointer, (const uint8_t *)src, bytes, s);
-    (void)hipGetLastError();       // a pageable pointer is an "invalid value" to the query
+    hipPointerAttribute_t ad, as;
+    if (query(&ad, dst) && ad.type == hipMemoryTypeHost && ad.devicePointer && query(&as, src) &&
+        as.type == hipMemoryTypeDevice && as.device == device)
+        return launch_store_host((uint8_t *)ad.devicePointer, (const uint8_t *)src, bytes, s);
     return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s);
 }
 
@@ -729,7 +737,7 @@ int rt_encrypt_host(const rt_keyset *k, const uint8_t *pt, const uint64_t *pt_of
         a.tok += tok_off[0]; a.tok_off = nullptr;
     }
     if ((rc = enc_common(k, a, s))) return rc;
-    RT_HIP(h ? launch_store_host(g.h_stage_dev + o_tok, w + o_tok, tok_ext, s) : copy_d2h(tok, w + o_tok, tok_ext, s),
+    RT_HIP(h ? launch_store_host(g.h_stage_dev + o_tok, w + o_tok, tok_ext, s) : copy_d2h(tok, w + o_tok, tok_ext, s, k->ctx->device),
            "D2H tok");
     RT_HIP(hipStreamSynchronize(s), "stream sync");
     g.stage_busy = false;
@@ -804,9 +812,9 @@ int rt_decrypt_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_
         memcpy(status, h + o_st, 4ull * n);
         return RT_OK;
     }
-    if (pt_ext) RT_HIP(copy_d2h(pt, w + o_pt, pt_ext, s), "D2H pt");
-    RT_HIP(copy_d2h(pt_len, w + o_ol, 4ull * n, s), "D2H pt_len");
-    RT_HIP(copy_d2h(status, w + o_st, 4ull * n, s), "D2H status");
+    if (pt_ext) RT_HIP(copy_d2h(pt, w + o_pt, pt_ext, s, k->ctx->device), "D2H pt");
+    RT_HIP(copy_d2h(pt_len, w + o_ol, 4ull * n, s, k->ctx->device), "D2H pt_len");
+    RT_HIP(copy_d2h(status, w + o_st, 4ull * n, s, k->ctx->device), "D2H status");
     RT_HIP(hipStreamSynchronize(s), "stream sync");
     return RT_OK;
 }
@@ -844,6 +852,11 @@ int rt_hdlc_deframe(rt_ctx *c, const uint8_t *buf, uint64_t len, uint32_t hw_mtu
     return RT_OK;
 }
 
+static bool overlaps(const void *a, const void *b, uint64_t a_bytes, uint64_t b_bytes = 0) {
+    const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+    return x < y + (b_bytes ? b_bytes : a_bytes) && y < x + a_bytes;
+}
+
 uint64_t rt_frames_compact_workspace_bytes(uint64_t max_pairs) { return frames_compact_workspace_bytes(max_pairs); }
 
 int rt_frames_compact(rt_ctx *c, const uint64_t *frame_off, const uint32_t *frame_len, const int32_t *status,
@@ -853,6 +866,12 @@ int rt_frames_compact(rt_ctx *c, const uint64_t *frame_off, const uint32_t *fram
     if (!counts || !n_frames) return fail(RT_E_INVAL, "rt_frames_compact: null counts/n_frames");
     if (max_pairs && (!frame_off || !frame_len || !status || !f_off || !f_len || !frame_pair || !workspace))
         return fail(RT_E_INVAL, "rt_frames_compact: null buffer");
+    // k_compact_write reads frame_off[k] / frame_len[k] while other threads
+    // write f_off[r] / f_len[r] for r <= k: in-place compaction would race
+    if (max_pairs && (overlaps(f_off, frame_off, 8 * max_pairs) || overlaps(f_len, frame_len, 4 * max_pairs) ||
+                      overlaps(f_off, frame_len, 8 * max_pairs, 4 * max_pairs) ||
+                      overlaps(f_len, frame_off, 4 * max_pairs, 8 * max_pairs)))
+        return fail(RT_E_INVAL, "rt_frames_compact: outputs must not overlap the frame arrays");
     RT_HIP(hipSetDevice(c->device), "hipSetDevice");
     RT_HIP(launch_frames_compact(frame_off, frame_len, status, counts, max_pairs, f_off, f_len, frame_pair, n_frames,
                                  workspace, pick(c, stream)),
@@ -1149,7 +1168,7 @@ int rt_verify_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_o
     a.tok = w + o_tok; a.tok_off = (const uint64_t *)(w + o_to); a.tok_len = (const uint32_t *)(w + o_tl);
     a.key_idx = key_idx ? (const uint32_t *)(w + o_ki) : nullptr; a.status = (int32_t *)(w + o_st); a.n = n;
     if ((rc = verify_common(k, a, s))) return rc;
-    RT_HIP(h ? launch_store_host(g.h_stage_dev + o_st, w + o_st, 4ull * n, s) : copy_d2h(status, w + o_st, 4ull * n, s),
+    RT_HIP(h ? launch_store_host(g.h_stage_dev + o_st, w + o_st, 4ull * n, s) : copy_d2h(status, w + o_st, 4ull * n, s, k->ctx->device),
            "D2H status");
     RT_HIP(hipStreamSynchronize(s), "stream sync");
     g.stage_busy = false;
@@ -1191,7 +1210,20 @@ int rt_memcpy_h2d(rt_ctx *c, void *dst, const void *src, uint64_t bytes, void *s
 int rt_memcpy_d2h(rt_ctx *c, void *dst, const void *src, uint64_t bytes, void *stream) {
     if (!c) return fail(RT_E_INVAL, "null context");
     RT_HIP(hipSetDevice(c->device), "hipSetDevice");
-    RT_HIP(copy_d2h(dst, src, bytes, pick(c, stream)), "D2H");
+    RT_HIP(copy_d2h(dst, src, bytes, pick(c, stream), c->device), "D2H");
+    return RT_OK;
+}
+int rt_memcpy_d2h_upto(rt_ctx *c, void *dst, const void *src, uint64_t max_bytes, const uint64_t *d_bytes,
+                       void *stream) {
+    if (!c || !dst || !src || !d_bytes) return fail(RT_E_INVAL, "rt_memcpy_d2h_upto: null argument");
+    RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+    hipPointerAttribute_t ad, as;
+    if (!(query(&ad, dst) && ad.type == hipMemoryTypeHost && ad.devicePointer && query(&as, src) &&
+          as.type == hipMemoryTypeDevice && as.device == c->device))
+        return fail(RT_E_INVAL, "rt_memcpy_d2h_upto: dst must be pinned host memory and src device memory of the "
+                                "context's GPU");
+    RT_HIP(launch_store_host((uint8_t *)ad.devicePointer, (const uint8_t *)src, max_bytes, pick(c, stream), d_bytes),
+           "D2H");
     return RT_OK;
 }
 int rt_stream_sync(rt_ctx *c, void *stream) {

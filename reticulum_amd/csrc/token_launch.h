@@ -142,7 +142,9 @@ hipError_t configure_kernels();
 // bytes from device memory `src` to pinned host memory, as GPU stores into the
 // mapped host buffer (dst_dev: its device-side address) on stream s
 // (copy_kernels.hip; faster than the copy engine's D2H, see there).
-hipError_t launch_store_host(uint8_t *dst_dev, const uint8_t *src, uint64_t bytes, hipStream_t s);
+// dev_bytes (device pointer, optional): copy min(bytes, *dev_bytes) bytes.
+hipError_t launch_store_host(uint8_t *dst_dev, const uint8_t *src, uint64_t bytes, hipStream_t s,
+                             const uint64_t *dev_bytes = nullptr);
 
 // Length bucketing: order[] = packet indices grouped by descending AES quad
 // count, so that the lanes of a wave carry similar lengths.  `dec` selects

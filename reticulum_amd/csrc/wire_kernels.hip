@@ -621,7 +621,7 @@ __device__ __forceinline__ void key_midstates(const uint8_t *key, uint32_t klen,
 // is raw[2:2+n], mask = HKDF(len, ifac, ifac_key) over everything but the
 // IFAC, reassembled [un0 & 0x7f, un1] || un[2+n:] (Transport.py:1441-1475).
 template <bool MASK>
-__global__ __launch_bounds__(256) void k_ifac(IfacArgs a) {
+__global__ __attribute__((amdgpu_waves_per_eu(4, 4))) __launch_bounds__(256) void k_ifac(IfacArgs a) {
     // the ifac_key midstates are the same for every packet: wave 0 computes
     // them once per workgroup (2 of a 500-B packet's 38 compressions)
     __shared__ uint32_t key_ms[16];
@@ -654,42 +654,93 @@ __global__ __launch_bounds__(256) void k_ifac(IfacArgs a) {
     const uint32_t total = MASK ? L + n : L;           // HKDF output length
     // HKDF (HKDF.py:35-62) with salt = ifac_key, ikm = ifac, no context:
     // PRK = HMAC(ifac_key, ifac); T_b = HMAC(PRK, T_{b-1} || b+1)
-    uint32_t hi[8], ho[8], prk[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { hi[k] = key_ms[k]; ho[k] = key_ms[8 + k]; }
-    {
-        uint32_t w[16], h[8];
-        // ifac_size <= 64: one or two message blocks after the ipad block
+    uint32_t phi[8], pho[8];
+    if constexpr (MASK) {
+        // PRK's blocks, its outer hash and PRK's two key midstates through ONE
+        // inlined compression (steps uniform across the wave: scalar branches):
+        // 4 % faster for the mask, 1.7 % slower for the unmask, whose early
+        // exit makes the steps divergent (profiles/r03as_ifac_site_ab/)
         const uint64_t bits = (64ull + n) * 8ull;
         const uint32_t nblk = (n + 8u) / 64u + 1u;
+        uint32_t st[8], prk[8];
+#pragma nounroll
+        for (uint32_t s = 0; s < nblk + 3u; ++s) {
+            uint32_t w[16], h[8];
+            if (s < nblk) {                       // PRK inner: ipad midstate, then the IFAC's blocks
 #pragma unroll
-        for (int k = 0; k < 8; ++k) h[k] = hi[k];
-        for (uint32_t b = 0; b < nblk; ++b) {
+                for (int k = 0; k < 8; ++k) h[k] = s == 0 ? key_ms[k] : st[k];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                uint32_t v = 0;
+                for (int k = 0; k < 16; ++k) {
+                    uint32_t v = 0;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t q = 64u * b + 4u * k + j;
-                    v = (v << 8) | (q < n ? ifac[q] : (q == n ? 0x80u : 0u));
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t q = 64u * s + 4u * k + j;
+                        v = (v << 8) | (q < n ? ifac[q] : (q == n ? 0x80u : 0u));
+                    }
+                    w[k] = v;
                 }
-                w[k] = v;
-            }
-            if (b + 1 == nblk) {
-                w[14] = (uint32_t)(bits >> 32);
-                w[15] = (uint32_t)bits;
+                if (s + 1 == nblk) {
+                    w[14] = (uint32_t)(bits >> 32);
+                    w[15] = (uint32_t)bits;
+                }
+            } else if (s == nblk) {               // PRK outer: opad midstate, inner digest
+#pragma unroll
+                for (int k = 0; k < 8; ++k) { h[k] = key_ms[8 + k]; w[k] = st[k]; }
+                w[8] = 0x80000000u;
+#pragma unroll
+                for (int k = 9; k < 15; ++k) w[k] = 0;
+                w[15] = (64 + 32) * 8;
+            } else {                              // PRK ^ ipad, PRK ^ opad
+                const uint32_t pad = s == nblk + 1u ? 0x36363636u : 0x5c5c5c5cu;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) { h[k] = SHA_IV[k]; w[k] = prk[k] ^ pad; w[8 + k] = pad; }
             }
             sha256_compress(h, w);
-        }
-        hmac_outer(prk, h, ho);
-    }
-    uint8_t prkb[32];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        prkb[4 * k] = prk[k] >> 24; prkb[4 * k + 1] = prk[k] >> 16; prkb[4 * k + 2] = prk[k] >> 8; prkb[4 * k + 3] = prk[k];
+            for (int k = 0; k < 8; ++k) {
+                if (s < nblk) st[k] = h[k];
+                else if (s == nblk) prk[k] = h[k];
+                else if (s == nblk + 1u) phi[k] = h[k];
+                else pho[k] = h[k];
+            }
+        }
+    } else {
+        uint32_t hi[8], ho[8], prk[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { hi[k] = key_ms[k]; ho[k] = key_ms[8 + k]; }
+        {
+            uint32_t w[16], h[8];
+            // ifac_size <= 64: one or two message blocks after the ipad block
+            const uint64_t bits = (64ull + n) * 8ull;
+            const uint32_t nblk = (n + 8u) / 64u + 1u;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) h[k] = hi[k];
+            for (uint32_t b = 0; b < nblk; ++b) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    uint32_t v = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t q = 64u * b + 4u * k + j;
+                        v = (v << 8) | (q < n ? ifac[q] : (q == n ? 0x80u : 0u));
+                    }
+                    w[k] = v;
+                }
+                if (b + 1 == nblk) {
+                    w[14] = (uint32_t)(bits >> 32);
+                    w[15] = (uint32_t)bits;
+                }
+                sha256_compress(h, w);
+            }
+            hmac_outer(prk, h, ho);
+        }
+        uint8_t prkb[32];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            prkb[4 * k] = prk[k] >> 24; prkb[4 * k + 1] = prk[k] >> 16; prkb[4 * k + 2] = prk[k] >> 8; prkb[4 * k + 3] = prk[k];
+        }
+        key_midstates(prkb, 32, phi, pho);
     }
-    uint32_t phi[8], pho[8];
-    key_midstates(prkb, 32, phi, pho);
     uint32_t t[8];
     for (uint32_t b = 0; 32u * b < total; ++b) {
         // message T_{b-1} (32 B, none for b = 0) || counter byte

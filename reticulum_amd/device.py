@@ -505,3 +505,24 @@ def copy_to_host(dst, src, stream=None):
     lib = _native.load()
     _native.check(lib.rt_memcpy_d2h(_ctx_of(src), dst.data_ptr(), src.data_ptr(), nbytes,
                                     _stream(stream, src.device)))
+
+
+def copy_to_host_upto(dst, src, nbytes_dev, stream=None):
+    """Enqueue the copy of the first min(dst size, nbytes_dev) bytes of the
+    device tensor ``src`` into the pinned host tensor ``dst``, where
+    ``nbytes_dev`` is a one-element int64 DEVICE tensor read at run time (e.g.
+    ``frame_off[n]`` from hdlc_frame: the stream's length, which the host
+    does not know without a sync) — GPU stores into the mapped buffer
+    (rt_memcpy_d2h_upto).  Nothing is synchronised."""
+    if not src.is_cuda or dst.is_cuda or not dst.is_pinned():
+        raise ValueError("copy_to_host_upto copies a device tensor into a pinned host tensor")
+    if not src.is_contiguous() or not dst.is_contiguous():
+        raise ValueError("copy_to_host_upto needs contiguous tensors")
+    if nbytes_dev.dtype != torch.int64 or nbytes_dev.numel() != 1 or not nbytes_dev.is_cuda:
+        raise TypeError("nbytes_dev: one int64 element on the device")
+    nbytes = min(src.numel() * src.element_size(), dst.numel() * dst.element_size())
+    if nbytes == 0:
+        return
+    lib = _native.load()
+    _native.check(lib.rt_memcpy_d2h_upto(_ctx_of(src), dst.data_ptr(), src.data_ptr(), nbytes, _p(nbytes_dev),
+                                         _stream(stream, src.device)))

@@ -42,7 +42,8 @@ def outbound(ks: KeySet, pt, iv, destination_hash, context, ifac, ifac_key, flag
     16), destination_hash (n, 16), context (n,) uint8, flags/hops (n,) uint8
     (default 0: HEADER_1 DATA, hop 0), ifac (n, ifac_size) the access codes
     (the tail of the interface identity's signature of each packet, made by
-    the caller), ifac_key (K,) uint8.  Returns (stream, frame_off): the HDLC
+    the caller; None or zero columns: an interface without IFAC, no mask),
+    ifac_key (K,) uint8 (unused without IFAC).  Returns (stream, frame_off): the HDLC
     byte stream is stream[:frame_off[n]] (int64 on the device), frame i at
     stream[frame_off[i]:frame_off[i+1]]."""
     with _on(stream):      # temporaries allocated on the stream that uses them
@@ -56,12 +57,17 @@ def outbound(ks: KeySet, pt, iv, destination_hash, context, ifac, ifac_key, flag
         off = torch.arange(n, dtype=torch.int64, device=dev) * pl
         flat = raw.view(-1)
         device.pack_headers(flags, hops, destination_hash, context, flat, off, stream=stream)
-        isz = ifac.shape[1]
-        ml = pl + isz
-        masked = torch.empty(n * ml, dtype=torch.uint8, device=dev)
-        m_off = torch.arange(n, dtype=torch.int64, device=dev) * ml
-        device.ifac_mask(flat, off, torch.full((n,), pl, dtype=torch.int32, device=dev), ifac, ifac_key, masked, m_off,
-                         stream=stream)
+        isz = ifac.shape[1] if ifac is not None else 0
+        if isz:
+            ml = pl + isz
+            masked = torch.empty(n * ml, dtype=torch.uint8, device=dev)
+            m_off = torch.arange(n, dtype=torch.int64, device=dev) * ml
+            device.ifac_mask(flat, off, torch.full((n,), pl, dtype=torch.int32, device=dev), ifac, ifac_key, masked,
+                             m_off, stream=stream)
+        else:
+            # an interface without IFAC transmits the packet as packed
+            # (Transport.py:1069-1071: the mask applies only with ifac_identity)
+            ml, masked, m_off = pl, flat, off
         framed = torch.empty(n * (2 * ml + 2), dtype=torch.uint8, device=dev)
         frame_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
         device.hdlc_frame(masked, m_off, torch.full((n,), ml, dtype=torch.int32, device=dev), framed, frame_off,
@@ -71,12 +77,15 @@ def outbound(ks: KeySet, pt, iv, destination_hash, context, ifac, ifac_key, flag
 
 def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stream=None):
     """One read of an interface's byte stream ``buf`` (uint8 on the device)
-    through deframing, IFAC unmask, unpack and token decrypt, for at most
+    through deframing, IFAC unmask (skipped for ``ifac_size`` 0, an interface
+    without access codes: then frames with the IFAC flag set are dropped, as
+    Transport.py:1482-1486 does), unpack and token decrypt, for at most
     ``max_pairs`` consecutive flag pairs (a stream of n frames has 2n - 1:
     frames and the empty gaps between them).
 
     Returns a dict of device tensors.  Per flag pair k: ``frame_status``
-    (RT_FRAME_*; -1 past the pairs found) and ``counts`` = [pairs, bytes
+    (RT_FRAME_*; -1 past the pairs found), ``frame_len`` (its unescaped
+    length) and ``counts`` = [pairs, bytes
     consumed] as the read loop leaves them (TCPInterface.py:391-411).  The
     frames the read loop hands on (RT_FRAME_OK) are compacted in stream order
     into the first ``n_frames`` (a device scalar) entries of the per-frame
@@ -102,11 +111,23 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
         frame_pair = torch.empty(max_pairs, dtype=torch.int64, device=dev)
         n_frames = torch.empty((), dtype=torch.int64, device=dev)
         device.frames_compact(d_off, d_len, d_st, counts, f_off, f_len, frame_pair, n_frames, stream=stream)
-        un = torch.empty_like(out)
         ifac = torch.empty((max_pairs, ifac_size), dtype=torch.uint8, device=dev)
-        ifac_status = torch.empty(max_pairs, dtype=torch.int32, device=dev)
-        p_len = torch.empty(max_pairs, dtype=torch.int32, device=dev)
-        device.ifac_unmask(out, f_off, f_len, ifac_key, ifac, un, f_off, ifac_status, out_len=p_len, stream=stream)
+        if ifac_size:
+            un = torch.empty_like(out)
+            ifac_status = torch.empty(max_pairs, dtype=torch.int32, device=dev)
+            p_len = torch.empty(max_pairs, dtype=torch.int32, device=dev)
+            device.ifac_unmask(out, f_off, f_len, ifac_key, ifac, un, f_off, ifac_status, out_len=p_len,
+                               stream=stream)
+        else:
+            # no IFAC on the interface: a packet with the IFAC flag set is
+            # dropped, the others go to unpack as they are
+            # (Transport.py:1482-1486); the empty entries past the frames
+            # (f_len 0) stay dropped
+            un = out
+            flagged = (out[f_off] & 0x80) != 0
+            drop = flagged | (f_len <= 2)
+            ifac_status = drop.to(torch.int32)
+            p_len = torch.where(drop, torch.zeros_like(f_len), f_len)
         fields = torch.empty((max_pairs, 96), dtype=torch.uint8, device=dev)
         device.packet_unpack(un, f_off, p_len, fields, stream=stream)
         tok_off = torch.empty(max_pairs, dtype=torch.int64, device=dev)
@@ -119,7 +140,7 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
         device.decrypt(ks, un, tok_off, tok_len, pt, tok_off, pt_len, status, stream=stream)
     return {"pt": pt, "pt_off": tok_off, "pt_len": pt_len, "status": status, "ifac": ifac,
             "ifac_status": ifac_status, "fields": fields, "frame_pair": frame_pair, "n_frames": n_frames,
-            "frame_status": d_st, "counts": counts}
+            "frame_status": d_st, "frame_len": d_len, "counts": counts}
 
 
 def _on(stream):

@@ -14,9 +14,17 @@ def _build():
     subprocess.run(["make", "-s", "-C", os.path.join(HERE, "c_host")], check=True, timeout=120)
 
 
+ROOT = os.path.dirname(HERE)
+LIBS = [os.path.join(ROOT, "reticulum_amd", "librnstok.so"), os.path.join(ROOT, "oracle", "liboracle_token.so")]
+
+
 def test_c_host_program_builds_against_the_header():
     """CPU: the program compiles with -Werror against include/rnstok.h and
-    links against librnstok.so (every symbol it calls is exported)."""
+    links against librnstok.so (every symbol it calls is exported).  Skipped
+    on a checkout where the libraries are not built (__graft_entry__.build())."""
+    missing = [p for p in LIBS if not os.path.exists(p)]
+    if missing:
+        pytest.skip("not built: " + ", ".join(os.path.relpath(p, ROOT) for p in missing))
     _build()
     assert os.access(BIN, os.X_OK)
 

@@ -141,7 +141,8 @@ enum {
     RT_KERNEL_GENERAL = 0,      /* one packet per lane (k_encrypt / k_decrypt) */
     RT_KERNEL_ENC_LONG4 = 1,    /* single key, a lane quad per CBC chain (k_encrypt_long4) */
     RT_KERNEL_ENC_LONG = 2,     /* per-packet keys, hashing on waves of their own (k_encrypt_long) */
-    RT_KERNEL_DEC_LONG2 = 3     /* single key, producer/consumer HMAC chains (k_decrypt_long2) */
+    RT_KERNEL_DEC_LONG2 = 3,    /* single key, producer/consumer HMAC chains (k_decrypt_long2) */
+    RT_KERNEL_ENC_SPLIT = 4     /* single key, AES and HMAC chains on waves of their own (k_encrypt_split) */
 };
 int         rt_plan_uniform(const rt_ctx *ctx, uint32_t n, uint32_t len, int per_packet_keys, int decrypt);
 

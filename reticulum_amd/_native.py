@@ -16,6 +16,7 @@ RT_OK, RT_E_INVAL, RT_E_HIP, RT_E_NOMEM, RT_E_NODEV = 0, -1, -2, -3, -4
 RT_F_SORT_BY_LENGTH = 1
 RT_ST_OK, RT_ST_TOO_SHORT, RT_ST_BAD_HMAC, RT_ST_BAD_CT_LEN, RT_ST_BAD_PAD = 0, 1, 2, 3, 4
 RT_KERNEL_GENERAL, RT_KERNEL_ENC_LONG4, RT_KERNEL_ENC_LONG, RT_KERNEL_DEC_LONG2 = 0, 1, 2, 3
+RT_KERNEL_ENC_SPLIT = 4
 
 # (name, restype, argtypes) for every entry point declared in include/rnstok.h
 _vp, _u32, _u64, _i32, _int = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int

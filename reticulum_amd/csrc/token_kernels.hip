@@ -309,6 +309,167 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
     }
 }
 
+// ----------------------------------------------------- encrypt, split roles --
+//
+// The same work as k_encrypt with the two chains on waves of their own
+// (VERDICT r03 next #2): waves 0..7 of the 1024-thread workgroup (two per
+// SIMD; wave w sits on SIMD w % 4) run the CBC chains of 64 packets each, one
+// per lane, and store the ciphertext; waves 8..15 (two per SIMD) hash it,
+// wave 8+k the packets of AES wave k on the same SIMD.  In register-only
+// loops this mix issues 19 % fewer SIMD-cycles per (AES quad + SHA-256
+// compression) than one wave carrying both chains (tools/floor_probe.hip
+// core_split8 10 188 vs core_enc 12 583, profiles/r04_split/r04b_floor_split.txt).
+//
+// Hand-over, two instances (A/B in one process against k_encrypt, tokens
+// identical, profiles/r04_split/r04f_three_way_ab.txt, r04h_enc_dec_split_ab.txt):
+// * packed rows (RB = false): an LDS ring after the 128 KiB table image, one
+//   slot of one quad per lane (4 KiB per AES wave, 16-B unit j of lane l at
+//   1024 j + 16 l: conflict-free ds_write_b128 / ds_read_b128), which fills
+//   the CU's 160 KiB.  The two hand-over counters of each wave pair live in
+//   lane 0's first unit, so lane 0's quad goes another way: the hashing wave's
+//   lane 0 reads it back from the token buffer.  500 B: 0.857 vs 0.891 ms
+//   (-3.8 %) and 0.839 vs 0.886 (-5.3 %) on two boxes; 1500 B -2.5 / -3.1 %.
+//   Reading every lane's quad back from the token rows instead (a second
+//   scattered 16-B pattern) is 1.6 % slower at 500 B.
+// * interleaved (RB = true): no ring, every hashing lane reads its quad back
+//   from the token buffer (coalesced 1-KiB reads, L2 hits, no LDS instruction
+//   taken from the lookups' pipe): 0.743 vs 0.814 ms (-8.8 %), 1500 B -9.6 %;
+//   the LDS ring there: -3.7 %.  (A staging ring in global memory instead of
+//   LDS: -2.4 % rows, -2.8 % interleaved: 4 more stores per quad, ring lines
+//   leaving L2; profiles/r04_split/r04d_global_stage_ab.txt.)
+// AES wave k stores quad q's ciphertext, writes it to its slot and publishes
+// its count of quads with a workgroup-scope release; hashing wave 8+k waits
+// for that count (s_sleep), reads the slot after an acquire and publishes its
+// own count, which the AES wave checks before it overwrites the slot.  One
+// slot is enough: the hashing wave takes a quad as soon as it is there unless
+// it is finishing a packet (3 compressions), which is shorter than two AES
+// quads.  Every wave leaves after the same batches, so the grid always
+// drains.  Single key, uniform lengths (rows at a stride, or ILV).
+constexpr uint32_t SPLIT_AES_WAVES = 8, SPLIT_THREADS = 1024;
+constexpr uint32_t SPLIT_RING = LDS_ENC_BYTES;                    // 8 x 4 KiB
+constexpr uint32_t LDS_ENC_SPLIT_BYTES = SPLIT_RING + SPLIT_AES_WAVES * 4096u;
+static_assert(LDS_ENC_SPLIT_BYTES <= 160u * 1024u, "LDS");
+
+template <int NR, bool ILV = false, bool RB = ILV>
+__global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
+    typedef __attribute__((address_space(3))) uint32_t lds_u32;
+    typedef __attribute__((address_space(3))) u32x4 lds_q;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const bool aes = wave < SPLIT_AES_WAVES;
+    const uint32_t pair = aes ? wave : wave - SPLIT_AES_WAVES;
+    const uint32_t slot = SPLIT_RING + 4096u * pair;
+    lds_u32 *produced = (lds_u32 *)(uintptr_t)slot, *consumed = (lds_u32 *)(uintptr_t)(slot + 4u);
+    if (aes && lane < 2u) ((lds_u32 *)(uintptr_t)slot)[lane] = 0u;   // before the barrier
+    fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);     // ends with the workgroup barrier
+
+    const uint32_t L = a.uni_len, nfull = L >> 4, nq = nfull >> 2, tb = (nfull & 3u) + 1u, rem = L & 15u;
+    const uint64_t US = ILV ? 16ull * a.n : 16ull;
+    const uint32_t n_batches = (a.n + 63u) >> 6;
+    const uint32_t first = blockIdx.x * SPLIT_AES_WAVES + pair, stride = gridDim.x * SPLIT_AES_WAVES;
+    lds_q *mine = (lds_q *)(uintptr_t)(slot + 16u * lane);     // unit j at mine[64 j]
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    uint32_t count = 0;                                    // quads handed over so far (both sides)
+    if (aes) {
+        const Lanes LN(threadIdx.x & 31u);
+        Keys<NR, false> K;
+        K.load(a.rec, REC_ENC);
+        Sha256 S;                                          // unused: enc_quad<NR, false> hashes nothing
+        for (uint32_t b = first; b < n_batches; b += stride) {
+            const uint32_t p = 64u * b + lane;
+            const bool valid = p < a.n;
+            const uint8_t *P = ILV ? a.pt + 16ull * p : a.pt + (uint64_t)p * a.pt_stride;
+            uint8_t *O = ILV ? a.tok + 16ull * p : a.tok + (uint64_t)p * a.tok_stride;
+            u32x4 prev = valid ? ld16(a.iv + 16ull * p) : z;
+            if (valid) st16(O, prev);
+            uint8_t *C = O + US;
+            for (uint32_t q = 0; q <= nq; ++q) {
+                u32x4 x[4], c[4];
+                if (q < nq) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) x[j] = valid ? ld16(P + US * j) : z;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        x[j] = !valid ? z
+                                      : ((uint32_t)j + 1u < tb ? ld16(P + US * j)
+                                                               : ((uint32_t)j + 1u == tb ? pad_block(P + US * j, rem) : z));
+                }
+                enc_quad<NR, false>(c, x, prev, K.rk, LN, S);
+                const uint32_t nst = q < nq ? 4u : tb;
+                if (valid) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if ((uint32_t)j < nst) st16(C + US * j, c[j]);
+                }
+                prev = c[3];
+                P += 4 * US;
+                C += 4 * US;
+                // the slot is free once the hashing wave has taken every earlier quad
+                if (!RB && count)
+                    while (__hip_atomic_load(consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < count)
+                        __builtin_amdgcn_s_sleep(1);
+                if (!RB && lane) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) mine[64 * j] = c[j];
+                }
+                ++count;
+                // lane 0's quad (read back from the token buffer) and the
+                // slot's writes before the count the hashing wave polls
+                if (lane == 0u) __hip_atomic_store(produced, count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+    } else {
+        for (uint32_t b = first; b < n_batches; b += stride) {
+            const uint32_t p = 64u * b + lane;
+            const bool valid = p < a.n;
+            uint8_t *O = ILV ? a.tok + 16ull * p : a.tok + (uint64_t)p * a.tok_stride;
+            const uint8_t *C = O + US;
+            uint32_t h[8];
+            load_uniform8(h, a.rec + REC_IPAD);
+            u32x4 up = valid ? ld16(a.iv + 16ull * p) : z;      // the unit before the quad (IV first)
+            uint32_t w[16];
+            for (uint32_t q = 0; q <= nq; ++q) {
+                while (__hip_atomic_load(produced, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < count + 1u)
+                    __builtin_amdgcn_s_sleep(1);
+                const uint32_t nst = q < nq ? 4u : tb;
+                u32x4 c[4];
+                if (!RB && lane) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) c[j] = mine[64 * j];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) c[j] = (valid && (uint32_t)j < nst) ? ld16(C + US * j) : z;
+                }
+                ++count;
+                // the slot's reads complete before the AES wave may overwrite it
+                if (!RB && lane == 0u)
+                    __hip_atomic_store(consumed, count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                C += 4 * US;
+                sha_units(w, up, c[0], c[1], c[2]);
+                if (q < nq) sha256_compress(h, w);
+                up = c[3];
+            }
+            // w: units u0..u3 of the tail quad, up = u4 (units past the
+            // packet's own are not hashed); tu = tb + 1 units are left for the
+            // inner hash (as k_encrypt's tail)
+            const uint32_t tu = tb + 1u;
+            uint32_t u4[16], fin[16], opad[8];
+            sha_units(u4, up, z, z, z);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) u4[k] = tu >= 4u ? u4[k] : w[k];
+            sha_final_block(fin, u4, tu >= 4u ? tu - 4u : tu, (uint64_t)(64u + 16u + 16u * (nfull + 1u)) * 8u);
+            load_uniform8(opad, a.rec + REC_OPAD);
+            hmac_finish(h, tu >= 4u ? 0u : 1u, w, fin, opad);
+            if (valid) {
+                uint8_t *T = O + US * (nfull + 2u);
+                st16(T, u32x4{bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3])});
+                st16(T + US, u32x4{bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7])});
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------- encrypt, long tokens --
 //
 // Few, long tokens (e.g. 16 KiB Resource segments sharded over 8 GPUs leave
@@ -1346,6 +1507,38 @@ static Shape shape_for(uint32_t n, int max_threads, int n_cu) {
     return {(int)g, (int)t};
 }
 
+#ifndef RNSTOK_SPLIT_ENC            // 0: every single-key uniform batch on k_encrypt (the A/B baseline)
+#define RNSTOK_SPLIT_ENC 1
+#endif
+#ifndef RNSTOK_SPLIT_ROWS_RB          // packed rows: LDS ring (0) or read-back (1)
+#define RNSTOK_SPLIT_ROWS_RB 0
+#endif
+#ifndef RNSTOK_SPLIT_ILV_RB           // interleaved: read-back (1) or LDS ring (0)
+#define RNSTOK_SPLIT_ILV_RB 1
+#endif
+// Split-role encrypt (k_encrypt_split): single key, uniform lengths, at least
+// one 64-packet batch per AES wave of every CU.
+static bool use_split_enc(const EncArgs &a, int n_cu) {
+    return RNSTOK_SPLIT_ENC && !a.key_idx && !a.pt_len && !a.order && !a.queue &&
+           (uint64_t)a.n >= 64ull * SPLIT_AES_WAVES * (uint64_t)n_cu;
+}
+static uint64_t split_grid(uint32_t n, int n_cu) {
+    const uint64_t batches = (n + 63ull) / 64ull;
+    uint64_t grid = (batches + SPLIT_AES_WAVES - 1) / SPLIT_AES_WAVES;
+    return grid > (uint64_t)n_cu ? (uint64_t)n_cu : grid;
+}
+template <int NR>
+static hipError_t launch_enc_split_nr(const EncArgs &a, int n_cu, hipStream_t s) {
+    const uint64_t grid = split_grid(a.n, n_cu);
+    if (a.ilv)
+        hipLaunchKernelGGL((k_encrypt_split<NR, true, RNSTOK_SPLIT_ILV_RB>), dim3((unsigned)grid), dim3(SPLIT_THREADS),
+                           LDS_ENC_SPLIT_BYTES, s, a);
+    else
+        hipLaunchKernelGGL((k_encrypt_split<NR, false, RNSTOK_SPLIT_ROWS_RB>), dim3((unsigned)grid),
+                           dim3(SPLIT_THREADS), LDS_ENC_SPLIT_BYTES, s, a);
+    return hipGetLastError();
+}
+
 template <int NR>
 static hipError_t launch_enc_nr(const EncArgs &a, Shape sh, hipStream_t s) {
     if (a.ilv && a.key_idx)
@@ -1444,6 +1637,9 @@ int plan_encrypt(uint32_t n, bool packed, uint32_t uni_len, bool per_key, int n_
     if (!per_key && use_long(n, len, uni_len, n_cu, RNSTOK_LONG_MIN_LEN)) return RT_KERNEL_ENC_LONG4;
 #endif
     if (use_long(n, len, uni_len, n_cu, RNSTOK_LONG_PERKEY_MIN_LEN)) return RT_KERNEL_ENC_LONG;
+    EncArgs a{};
+    a.n = n; a.uni_len = uni_len; a.pt_len = len; a.key_idx = per_key ? &uni_len : nullptr;
+    if (use_split_enc(a, n_cu)) return RT_KERNEL_ENC_SPLIT;
     return RT_KERNEL_GENERAL;
 }
 
@@ -1455,6 +1651,8 @@ hipError_t launch_encrypt(const EncArgs &args, int nr, int n_cu, SpareQueue *spa
     if (plan == RT_KERNEL_ENC_LONG)
         return nr == 14 ? launch_enc_long_nr<14>(a, n_cu, s) : launch_enc_long_nr<10>(a, n_cu, s);
 
+    if (use_split_enc(a, n_cu))
+        return nr == 14 ? launch_enc_split_nr<14>(a, n_cu, s) : launch_enc_split_nr<10>(a, n_cu, s);
     const Shape sh = shape_for(a.n, a.key_idx ? WG_PERKEY_ENC : WG_ENC, n_cu);
     bool took = false;
     uint32_t slot = 0;
@@ -1537,6 +1735,10 @@ hipError_t configure_kernels() {
     RT_CFG((k_decrypt<10, false, WG_DEC, true>), LDS_DEC_BYTES);
     RT_CFG((k_decrypt<10, false, 1024, true>), LDS_DEC_BYTES);
     RT_CFG((k_decrypt<10, true, WG_PERKEY_DEC, true>), LDS_DEC_BYTES);
+    RT_CFG((k_encrypt_split<14, false, RNSTOK_SPLIT_ROWS_RB>), LDS_ENC_SPLIT_BYTES);
+    RT_CFG((k_encrypt_split<14, true, RNSTOK_SPLIT_ILV_RB>), LDS_ENC_SPLIT_BYTES);
+    RT_CFG((k_encrypt_split<10, false, RNSTOK_SPLIT_ROWS_RB>), LDS_ENC_SPLIT_BYTES);
+    RT_CFG((k_encrypt_split<10, true, RNSTOK_SPLIT_ILV_RB>), LDS_ENC_SPLIT_BYTES);
 #undef RT_CFG
     return e;
 }

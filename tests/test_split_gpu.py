@@ -1,0 +1,133 @@
+"""The split-role encrypt kernel (k_encrypt_split: AES chains and HMAC chains
+on waves of their own, the ciphertext handed over through an LDS ring or read
+back) at the batch sizes that route to it (at least 512 packets per CU, single
+key, uniform lengths), in both HBM layouts: tokens against the C oracle
+(Token.encrypt, Token.py:87-97) and identical between the layouts, every
+packet round-tripped, ragged last batches included; and decrypt's failures
+(Token.py:100-114) at the same sizes — tampered tokens (BAD_HMAC, plaintext
+zeroed), authentic tokens with a bad pad byte (BAD_PAD) — exactly where the
+oracle puts them (k_decrypt_split was measured and not adopted, but these
+shapes guard whichever decrypt kernel runs there)."""
+import hashlib
+import hmac as _hmac
+
+import numpy as np
+import pytest
+
+from oracle import ctoken as oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rt():
+    import reticulum_amd
+    from reticulum_amd import _native
+    assert _native.load().rt_device_count() >= 1, "no HIP device visible"
+    _native.context(0)
+    return reticulum_amd
+
+
+def _split_n(extra):
+    from reticulum_amd import _native
+    n_cu = _native.load().rt_num_cus(_native.context(0))
+    return 64 * 8 * n_cu + extra
+
+
+@pytest.mark.parametrize("L,klen,extra", [(500, 64, 0), (500, 64, 37), (0, 64, 5), (15, 64, 63), (16, 32, 64),
+                                          (17, 64, 1), (100, 32, 0), (1500, 64, 129), (63, 64, 3)])
+def test_split_kernels_tokens_and_round_trip(rt, L, klen, extra):
+    import torch
+    from reticulum_amd import _native, device
+    n = _split_n(extra)
+    lib, ctx = _native.load(), _native.context(0)
+    tl = rt.token_len(L)
+    assert lib.rt_plan_uniform(ctx, n, L, 0, 0) == _native.RT_KERNEL_ENC_SPLIT
+    assert lib.rt_plan_uniform(ctx, n - extra - 1, L, 0, 0) == _native.RT_KERNEL_GENERAL
+    rng = np.random.Generator(np.random.PCG64(1000 + L + extra))
+    key = rng.integers(0, 256, klen, dtype=np.uint8).tobytes()
+    ks = rt.KeySet(key)
+    g = torch.Generator(device="cuda").manual_seed(L + 7)
+    pt = torch.randint(0, 256, (n, max(L, 1)), dtype=torch.uint8, device="cuda", generator=g)[:, :L]
+    iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
+    tok = torch.full((n, tl), 0xEE, dtype=torch.uint8, device="cuda")
+    device.encrypt_uniform(ks, pt, L, iv, tok)
+    tu = torch.full((tl // 16, n, 16), 0xEE, dtype=torch.uint8, device="cuda")
+    device.encrypt_interleaved(ks, device.interleave(pt, L), L, iv, tu)
+    torch.cuda.synchronize()
+    assert torch.equal(device.deinterleave(tu, tl), tok)
+    t_h, p_h, iv_h = tok.cpu().numpy(), pt.cpu().numpy(), iv.cpu().numpy()
+    sel = np.unique(np.concatenate([[0, 63, 64, n - 65, n - 1], rng.integers(0, n, 40)]))
+    for i in sel:
+        assert t_h[i].tobytes() == oracle.encrypt(key, iv_h[i].tobytes(), p_h[i].tobytes()), i
+    # round trip through both layouts
+    back = torch.full((n, tl - 48), 0x55, dtype=torch.uint8, device="cuda")
+    ol = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    device.decrypt_uniform(ks, tok, tl, back, ol, st)
+    bu = torch.full(((tl - 48) // 16, n, 16), 0x55, dtype=torch.uint8, device="cuda")
+    ol2, st2 = torch.empty_like(ol), torch.empty_like(st)
+    device.decrypt_interleaved(ks, tu, tl, bu, ol2, st2)
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0 and bool((ol == L).all()) and torch.equal(back[:, :L], pt)
+    assert torch.equal(st2, st) and torch.equal(ol2, ol) and torch.equal(device.deinterleave(bu, tl - 48), back)
+
+
+@pytest.mark.parametrize("layout", ["rows", "interleaved"])
+def test_split_decrypt_failures_match_the_oracle(rt, layout):
+    """1 % tampered tokens (tag, ciphertext, IV bytes) and authentic tokens
+    whose last plaintext byte is above 16, spread over the batches of a
+    split-size batch: statuses, lengths and zeroed plaintexts as the oracle's."""
+    import torch
+    from reticulum_amd import _native, device
+    rng = np.random.Generator(np.random.PCG64(4242 + (layout == "rows")))
+    n = _split_n(45)
+    L = 50                                   # 4 ciphertext blocks: the forged bad-pad tokens' shape
+    tl = rt.token_len(L)
+    assert tl == 16 + 64 + 32
+    lib, ctx = _native.load(), _native.context(0)
+    key = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+    ks = rt.KeySet(key)
+    pt = torch.from_numpy(rng.integers(0, 256, (n, L), dtype=np.uint8)).cuda()
+    iv = torch.from_numpy(rng.integers(0, 256, (n, 16), dtype=np.uint8)).cuda()
+    tok = torch.empty((n, tl), dtype=torch.uint8, device="cuda")
+    device.encrypt_uniform(ks, pt, L, iv, tok)
+    torch.cuda.synchronize()
+    t = tok.cpu().numpy()
+    bad = rng.choice(n, n // 100, replace=False)
+    for j, i in enumerate(bad):
+        t[i, int(rng.integers(0, tl))] ^= 1 << int(j % 8)
+    rest = np.setdiff1d(np.arange(n), bad)
+    forged_at = rng.choice(rest, 40, replace=False)
+    last = {}
+    for i in forged_at:                      # authentic, last byte 0x11..0xff (> 16)
+        last[int(i)] = int(rng.integers(17, 256))
+        body = bytes(rng.integers(0, 256, 63, dtype=np.uint8)) + bytes([last[int(i)]])
+        f = oracle.encrypt(key, bytes(rng.integers(0, 256, 16, dtype=np.uint8)), body)
+        ivb, ct = f[:16], f[16:-32][:-16]    # drop the pad block
+        t[i] = np.frombuffer(ivb + ct + _hmac.new(key[:32], ivb + ct, hashlib.sha256).digest(), np.uint8)
+    tok2 = torch.from_numpy(t).cuda()
+    ol = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    if layout == "rows":
+        out = torch.full((n, tl - 48), 0x33, dtype=torch.uint8, device="cuda")
+        device.decrypt_uniform(ks, tok2, tl, out, ol, st)
+        torch.cuda.synchronize()
+        back = out.cpu().numpy()
+    else:
+        bu = torch.full(((tl - 48) // 16, n, 16), 0x33, dtype=torch.uint8, device="cuda")
+        device.decrypt_interleaved(ks, device.interleave(tok2, tl), tl, bu, ol, st)
+        torch.cuda.synchronize()
+        back = device.deinterleave(bu, tl - 48).cpu().numpy()
+    st_h, ol_h = st.cpu().numpy(), ol.cpu().numpy()
+    want_bad = set(int(i) for i in bad)
+    assert set(np.nonzero(st_h == 2)[0].tolist()) == want_bad
+    assert set(np.nonzero(st_h == 4)[0].tolist()) == set(int(i) for i in forged_at)
+    for i in list(bad[:30]) + list(forged_at[:10]):
+        s, p = oracle.decrypt(key, t[i].tobytes())
+        assert st_h[i] == s and not back[i].any(), i
+    for i in forged_at:
+        assert ol_h[i] == last[int(i)] and st_h[i] == 4      # the authenticated pad byte
+    ok = st_h == 0
+    assert (ol_h[ok] == L).all()
+    assert np.array_equal(back[ok, :L], pt.cpu().numpy()[ok])

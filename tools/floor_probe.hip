@@ -262,6 +262,102 @@ __global__ __launch_bounds__(1024) void k_core_sha(const uint32_t *rec, uint32_t
     STAMP_END(acc)
 }
 
+// Split roles: waves [0, AW) run the AES chain alone
+// (enc_quad<14, false>, `iters` quads each), waves [AW, 16) the SHA-256
+// compressions alone (iters * AW / (16 - AW) each), so the SIMDs carry the
+// same work as k_core_enc's 16 x iters mixed quads.  Wave w sits on SIMD w % 4.
+template <int AW>
+__global__ __launch_bounds__(1024) void k_core_split(const uint32_t *rec, uint32_t *out, Stamp *st, uint32_t seed,
+                                                     int iters) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
+    fill_any(tab, LDS_ENC_BYTES / 4, seed);
+    const Lanes LN(threadIdx.x & 31u);
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t t = threadIdx.x * 0x9E3779B9u ^ seed;
+    uint32_t acc = 0;
+    STAMP_BEGIN()
+    if (wave < (uint32_t)AW) {
+        uint32_t rk[60];
+#pragma unroll
+        for (int i = 0; i < 60; ++i) rk[i] = __builtin_amdgcn_readfirstlane(rec[i]);
+        u32x4 x[4], c[4], prev = {t, t + 1, t + 2, t + 3};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[j] = u32x4{t ^ j, t + 7 * j, t * 3 + j, t ^ (j << 9)};
+        Sha256 S;
+#pragma nounroll
+        for (int i = 0; i < iters; ++i) {
+            enc_quad<14, false>(c, x, prev, rk, LN, S);
+            prev = c[3];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[j] = c[j] ^ x[j];
+        }
+        acc = prev.x ^ prev.y ^ prev.z ^ prev.w;
+    } else {
+        uint32_t h[8], w[16];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) h[k] = rec[k] ^ t;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = t + 3 * k;
+        const int n = iters * AW / (16 - AW);
+#pragma nounroll
+        for (int i = 0; i < n; ++i) {
+            sha256_compress(h, w);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) w[k] ^= h[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc ^= h[k];
+    }
+    STAMP_END(acc)
+}
+
+// The same split for decryption: waves [0, AW) dec_quad<14, false> (4
+// independent blocks, no SHA), waves [AW, 16) the compressions.
+template <int AW>
+__global__ __launch_bounds__(1024) void k_core_dsplit(const uint32_t *rec, uint32_t *out, Stamp *st, uint32_t seed,
+                                                      int iters) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
+    fill_any(tab, LDS_DEC_BYTES / 4, seed);
+    const Lanes LN(threadIdx.x & 31u);
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t t = threadIdx.x * 0x9E3779B9u ^ seed;
+    uint32_t acc = 0;
+    STAMP_BEGIN()
+    if (wave < (uint32_t)AW) {
+        uint32_t rk[60];
+#pragma unroll
+        for (int i = 0; i < 60; ++i) rk[i] = __builtin_amdgcn_readfirstlane(rec[i]);
+        u32x4 c[4], pp[4], prev = {t, t + 1, t + 2, t + 3};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[j] = u32x4{t ^ j, t + 7 * j, t * 3 + j, t ^ (j << 9)};
+        Sha256 S;
+#pragma nounroll
+        for (int i = 0; i < iters; ++i) {
+            dec_quad<14, false>(pp, c, prev, rk, LN, S);
+            prev = c[3];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) c[j] = c[j] ^ pp[j];
+        }
+        acc = prev.x ^ prev.y ^ prev.z ^ prev.w;
+    } else {
+        uint32_t h[8], w[16];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) h[k] = rec[k] ^ t;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = t + 3 * k;
+        const int n = iters * AW / (16 - AW);
+#pragma nounroll
+        for (int i = 0; i < n; ++i) {
+            sha256_compress(h, w);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) w[k] ^= h[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc ^= h[k];
+    }
+    STAMP_END(acc)
+}
+
 typedef void (*kfn)(const uint32_t *, uint32_t *, Stamp *, uint32_t, int);
 static int ncu;
 static uint32_t *d_out, *d_rec;
@@ -322,6 +418,25 @@ int main() {
     run("core_dec", k_core_dec<1024>, 1024, LDS_DEC_BYTES, IQ);
     const double cs = run("core_sha", k_core_sha, 1024, LDS_ENC_BYTES, IS);
     // 2 packets per lane at 2 waves/SIMD: per-packet cost = cycles per wave-iteration / 2
+    // split roles: per wave-iteration figures are per AES quad of the AES
+    // waves; the SIMD carries AW/4 AES waves, so per mixed-quad-equivalent:
+    // cycles * 4 waves / (AW/4 waves) ... printed as SIMD-cycles per quad+compression
+    for (int aw : {8, 10, 12}) {
+        kfn k = aw == 8 ? k_core_split<8> : (aw == 10 ? k_core_split<10> : k_core_split<12>);
+        char nm[32];
+        snprintf(nm, sizeof nm, "core_split%d", aw);
+        const double per = run(nm, k, 1024, LDS_ENC_BYTES, IQ);
+        printf("  split %d AES + %d SHA waves: %.0f SIMD-cycles per (AES quad + compression), mixed core_enc %.0f\n",
+               aw, 16 - aw, per * 16.0 / aw, qe);
+    }
+    for (int aw : {8, 10, 12}) {
+        kfn k = aw == 8 ? k_core_dsplit<8> : (aw == 10 ? k_core_dsplit<10> : k_core_dsplit<12>);
+        char nm[32];
+        snprintf(nm, sizeof nm, "core_dsplit%d", aw);
+        const double per = run(nm, k, 1024, LDS_DEC_BYTES, IQ);
+        printf("  dsplit %d AES + %d SHA waves: %.0f SIMD-cycles per (AES dec quad + compression), mixed core_dec %.0f\n",
+               aw, 16 - aw, per * 16.0 / aw, qd);
+    }
     const double x2s = run("core_enc_x2", k_core_enc_x2<false>, 512, LDS_ENC_BYTES, IQ);
     const double x2v = run("core_enc_x2vk", k_core_enc_x2<true>, 512, LDS_ENC_BYTES, IQ);
     printf("two packets per lane: %.0f (SGPR keys) / %.0f (VGPR keys) SIMD-cycles per packet-quad, against %.0f\n",

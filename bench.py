@@ -965,10 +965,10 @@ def sustained_clock_ghz(kernel, n, L, keys, layout="rows"):
     if not path:
         return None
     stats = path.replace("_ilvpmc.json", "_ilv_kernel_stats.csv").replace("_pmc.json", "_kernel_stats.csv")
-    tag = "k_encrypt<14, " if kernel == "encrypt" else "k_decrypt<14, "
+    tags = ("k_encrypt<14, ", "k_encrypt_split<14, ") if kernel == "encrypt" else ("k_decrypt<14, ",)
     try:
         with open(stats) as f:
-            rows = [r for r in csv.DictReader(f) if tag in r["Name"]]
+            rows = [r for r in csv.DictReader(f) if any(t in r["Name"] for t in tags)]
         ns = float(rows[0]["AverageNs"])
         return d[kernel]["GRBM_GUI_ACTIVE"] / 8 / ns
     except (OSError, KeyError, IndexError, ValueError):

@@ -344,13 +344,16 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
 // slot is enough: the hashing wave takes a quad as soon as it is there unless
 // it is finishing a packet (3 compressions), which is shorter than two AES
 // quads.  Every wave leaves after the same batches, so the grid always
-// drains.  Single key, uniform lengths (rows at a stride, or ILV).
+// drains.  Uniform lengths (rows at a stride, or ILV), one key or per-packet
+// keys (PERKEY: each AES lane loads its packet's round keys, each hashing lane
+// its ipad/opad midstates, from the 544-B key records; 128 VGPRs, 2 spilled
+// on rows).
 constexpr uint32_t SPLIT_AES_WAVES = 8, SPLIT_THREADS = 1024;
 constexpr uint32_t SPLIT_RING = LDS_ENC_BYTES;                    // 8 x 4 KiB
 constexpr uint32_t LDS_ENC_SPLIT_BYTES = SPLIT_RING + SPLIT_AES_WAVES * 4096u;
 static_assert(LDS_ENC_SPLIT_BYTES <= 160u * 1024u, "LDS");
 
-template <int NR, bool ILV = false, bool RB = ILV>
+template <int NR, bool ILV = false, bool RB = ILV, bool PERKEY = false>
 __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
     typedef __attribute__((address_space(3))) uint32_t lds_u32;
@@ -372,12 +375,13 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
     uint32_t count = 0;                                    // quads handed over so far (both sides)
     if (aes) {
         const Lanes LN(threadIdx.x & 31u);
-        Keys<NR, false> K;
-        K.load(a.rec, REC_ENC);
+        Keys<NR, PERKEY> K;
+        if (!PERKEY) K.load(a.rec, REC_ENC);
         Sha256 S;                                          // unused: enc_quad<NR, false> hashes nothing
         for (uint32_t b = first; b < n_batches; b += stride) {
             const uint32_t p = 64u * b + lane;
             const bool valid = p < a.n;
+            if (PERKEY) K.load(a.rec + (uint64_t)a.key_idx[valid ? p : 0u] * REC_WORDS, REC_ENC);
             const uint8_t *P = ILV ? a.pt + 16ull * p : a.pt + (uint64_t)p * a.pt_stride;
             uint8_t *O = ILV ? a.tok + 16ull * p : a.tok + (uint64_t)p * a.tok_stride;
             u32x4 prev = valid ? ld16(a.iv + 16ull * p) : z;
@@ -426,7 +430,11 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
             uint8_t *O = ILV ? a.tok + 16ull * p : a.tok + (uint64_t)p * a.tok_stride;
             const uint8_t *C = O + US;
             uint32_t h[8];
-            load_uniform8(h, a.rec + REC_IPAD);
+            const uint32_t *r = PERKEY ? a.rec + (uint64_t)a.key_idx[valid ? p : 0u] * REC_WORDS : a.rec;
+            if (PERKEY)
+                load8(h, r + REC_IPAD);
+            else
+                load_uniform8(h, a.rec + REC_IPAD);
             u32x4 up = valid ? ld16(a.iv + 16ull * p) : z;      // the unit before the quad (IV first)
             uint32_t w[16];
             for (uint32_t q = 0; q <= nq; ++q) {
@@ -459,7 +467,10 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
 #pragma unroll
             for (int k = 0; k < 16; ++k) u4[k] = tu >= 4u ? u4[k] : w[k];
             sha_final_block(fin, u4, tu >= 4u ? tu - 4u : tu, (uint64_t)(64u + 16u + 16u * (nfull + 1u)) * 8u);
-            load_uniform8(opad, a.rec + REC_OPAD);
+            if (PERKEY)
+                load8(opad, r + REC_OPAD);
+            else
+                load_uniform8(opad, a.rec + REC_OPAD);
             hmac_finish(h, tu >= 4u ? 0u : 1u, w, fin, opad);
             if (valid) {
                 uint8_t *T = O + US * (nfull + 2u);
@@ -1516,10 +1527,13 @@ static Shape shape_for(uint32_t n, int max_threads, int n_cu) {
 #ifndef RNSTOK_SPLIT_ILV_RB           // interleaved: read-back (1) or LDS ring (0)
 #define RNSTOK_SPLIT_ILV_RB 1
 #endif
-// Split-role encrypt (k_encrypt_split): single key, uniform lengths, at least
-// one 64-packet batch per AES wave of every CU.
+// Split-role encrypt (k_encrypt_split): uniform lengths, at least one
+// 64-packet batch per AES wave of every CU.
+#ifndef RNSTOK_SPLIT_PERKEY          // per-packet keys (c3) on the split kernel too: 0.845 vs 0.912 ms rows,
+#define RNSTOK_SPLIT_PERKEY 1        // 0.770 vs 0.852 interleaved (profiles/r04_split/r04i_perkey_ab.txt)
+#endif
 static bool use_split_enc(const EncArgs &a, int n_cu) {
-    return RNSTOK_SPLIT_ENC && !a.key_idx && !a.pt_len && !a.order && !a.queue &&
+    return RNSTOK_SPLIT_ENC && (!a.key_idx || RNSTOK_SPLIT_PERKEY) && !a.pt_len && !a.order && !a.queue &&
            (uint64_t)a.n >= 64ull * SPLIT_AES_WAVES * (uint64_t)n_cu;
 }
 static uint64_t split_grid(uint32_t n, int n_cu) {
@@ -1530,12 +1544,18 @@ static uint64_t split_grid(uint32_t n, int n_cu) {
 template <int NR>
 static hipError_t launch_enc_split_nr(const EncArgs &a, int n_cu, hipStream_t s) {
     const uint64_t grid = split_grid(a.n, n_cu);
-    if (a.ilv)
-        hipLaunchKernelGGL((k_encrypt_split<NR, true, RNSTOK_SPLIT_ILV_RB>), dim3((unsigned)grid), dim3(SPLIT_THREADS),
-                           LDS_ENC_SPLIT_BYTES, s, a);
+#define RT_SPLIT(ILV_, RB_, PK_)                                                                            \
+    hipLaunchKernelGGL((k_encrypt_split<NR, ILV_, RB_, PK_>), dim3((unsigned)grid), dim3(SPLIT_THREADS), \
+                       LDS_ENC_SPLIT_BYTES, s, a)
+    if (a.ilv && a.key_idx)
+        RT_SPLIT(true, RNSTOK_SPLIT_ILV_RB, true);
+    else if (a.ilv)
+        RT_SPLIT(true, RNSTOK_SPLIT_ILV_RB, false);
+    else if (a.key_idx)
+        RT_SPLIT(false, RNSTOK_SPLIT_ROWS_RB, true);
     else
-        hipLaunchKernelGGL((k_encrypt_split<NR, false, RNSTOK_SPLIT_ROWS_RB>), dim3((unsigned)grid),
-                           dim3(SPLIT_THREADS), LDS_ENC_SPLIT_BYTES, s, a);
+        RT_SPLIT(false, RNSTOK_SPLIT_ROWS_RB, false);
+#undef RT_SPLIT
     return hipGetLastError();
 }
 
@@ -1735,10 +1755,14 @@ hipError_t configure_kernels() {
     RT_CFG((k_decrypt<10, false, WG_DEC, true>), LDS_DEC_BYTES);
     RT_CFG((k_decrypt<10, false, 1024, true>), LDS_DEC_BYTES);
     RT_CFG((k_decrypt<10, true, WG_PERKEY_DEC, true>), LDS_DEC_BYTES);
-    RT_CFG((k_encrypt_split<14, false, RNSTOK_SPLIT_ROWS_RB>), LDS_ENC_SPLIT_BYTES);
-    RT_CFG((k_encrypt_split<14, true, RNSTOK_SPLIT_ILV_RB>), LDS_ENC_SPLIT_BYTES);
-    RT_CFG((k_encrypt_split<10, false, RNSTOK_SPLIT_ROWS_RB>), LDS_ENC_SPLIT_BYTES);
-    RT_CFG((k_encrypt_split<10, true, RNSTOK_SPLIT_ILV_RB>), LDS_ENC_SPLIT_BYTES);
+    RT_CFG((k_encrypt_split<14, false, RNSTOK_SPLIT_ROWS_RB, false>), LDS_ENC_SPLIT_BYTES);
+    RT_CFG((k_encrypt_split<14, true, RNSTOK_SPLIT_ILV_RB, false>), LDS_ENC_SPLIT_BYTES);
+    RT_CFG((k_encrypt_split<10, false, RNSTOK_SPLIT_ROWS_RB, false>), LDS_ENC_SPLIT_BYTES);
+    RT_CFG((k_encrypt_split<10, true, RNSTOK_SPLIT_ILV_RB, false>), LDS_ENC_SPLIT_BYTES);
+    RT_CFG((k_encrypt_split<14, false, RNSTOK_SPLIT_ROWS_RB, true>), LDS_ENC_SPLIT_BYTES);
+    RT_CFG((k_encrypt_split<14, true, RNSTOK_SPLIT_ILV_RB, true>), LDS_ENC_SPLIT_BYTES);
+    RT_CFG((k_encrypt_split<10, false, RNSTOK_SPLIT_ROWS_RB, true>), LDS_ENC_SPLIT_BYTES);
+    RT_CFG((k_encrypt_split<10, true, RNSTOK_SPLIT_ILV_RB, true>), LDS_ENC_SPLIT_BYTES);
 #undef RT_CFG
     return e;
 }

@@ -34,40 +34,44 @@ def _split_n(extra):
     return 64 * 8 * n_cu + extra
 
 
-@pytest.mark.parametrize("L,klen,extra", [(500, 64, 0), (500, 64, 37), (0, 64, 5), (15, 64, 63), (16, 32, 64),
-                                          (17, 64, 1), (100, 32, 0), (1500, 64, 129), (63, 64, 3)])
-def test_split_kernels_tokens_and_round_trip(rt, L, klen, extra):
+@pytest.mark.parametrize("L,klen,extra,n_keys", [(500, 64, 0, 1), (500, 64, 37, 1), (0, 64, 5, 1), (15, 64, 63, 1),
+                                                 (16, 32, 64, 1), (17, 64, 1, 1), (100, 32, 0, 1), (1500, 64, 129, 1),
+                                                 (63, 64, 3, 1), (500, 64, 11, 97), (100, 32, 64, 5), (1, 64, 0, 65536)])
+def test_split_kernels_tokens_and_round_trip(rt, L, klen, extra, n_keys):
     import torch
     from reticulum_amd import _native, device
     n = _split_n(extra)
     lib, ctx = _native.load(), _native.context(0)
     tl = rt.token_len(L)
-    assert lib.rt_plan_uniform(ctx, n, L, 0, 0) == _native.RT_KERNEL_ENC_SPLIT
-    assert lib.rt_plan_uniform(ctx, n - extra - 1, L, 0, 0) == _native.RT_KERNEL_GENERAL
-    rng = np.random.Generator(np.random.PCG64(1000 + L + extra))
-    key = rng.integers(0, 256, klen, dtype=np.uint8).tobytes()
-    ks = rt.KeySet(key)
+    pk = int(n_keys > 1)
+    assert lib.rt_plan_uniform(ctx, n, L, pk, 0) == _native.RT_KERNEL_ENC_SPLIT
+    assert lib.rt_plan_uniform(ctx, n - extra - 1, L, pk, 0) == _native.RT_KERNEL_GENERAL
+    rng = np.random.Generator(np.random.PCG64(1000 + L + extra + n_keys))
+    keys = rng.integers(0, 256, (n_keys, klen), dtype=np.uint8)
+    ks = rt.KeySet(keys if n_keys > 1 else keys[0].tobytes())
+    kidx = torch.from_numpy(rng.integers(0, n_keys, n).astype(np.int32)).cuda() if n_keys > 1 else None
     g = torch.Generator(device="cuda").manual_seed(L + 7)
     pt = torch.randint(0, 256, (n, max(L, 1)), dtype=torch.uint8, device="cuda", generator=g)[:, :L]
     iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
     tok = torch.full((n, tl), 0xEE, dtype=torch.uint8, device="cuda")
-    device.encrypt_uniform(ks, pt, L, iv, tok)
+    device.encrypt_uniform(ks, pt, L, iv, tok, key_idx=kidx)
     tu = torch.full((tl // 16, n, 16), 0xEE, dtype=torch.uint8, device="cuda")
-    device.encrypt_interleaved(ks, device.interleave(pt, L), L, iv, tu)
+    device.encrypt_interleaved(ks, device.interleave(pt, L), L, iv, tu, key_idx=kidx)
     torch.cuda.synchronize()
     assert torch.equal(device.deinterleave(tu, tl), tok)
     t_h, p_h, iv_h = tok.cpu().numpy(), pt.cpu().numpy(), iv.cpu().numpy()
+    kx = kidx.cpu().numpy() if kidx is not None else np.zeros(n, np.int64)
     sel = np.unique(np.concatenate([[0, 63, 64, n - 65, n - 1], rng.integers(0, n, 40)]))
     for i in sel:
-        assert t_h[i].tobytes() == oracle.encrypt(key, iv_h[i].tobytes(), p_h[i].tobytes()), i
+        assert t_h[i].tobytes() == oracle.encrypt(keys[kx[i]].tobytes(), iv_h[i].tobytes(), p_h[i].tobytes()), i
     # round trip through both layouts
     back = torch.full((n, tl - 48), 0x55, dtype=torch.uint8, device="cuda")
     ol = torch.empty(n, dtype=torch.int32, device="cuda")
     st = torch.empty(n, dtype=torch.int32, device="cuda")
-    device.decrypt_uniform(ks, tok, tl, back, ol, st)
+    device.decrypt_uniform(ks, tok, tl, back, ol, st, key_idx=kidx)
     bu = torch.full(((tl - 48) // 16, n, 16), 0x55, dtype=torch.uint8, device="cuda")
     ol2, st2 = torch.empty_like(ol), torch.empty_like(st)
-    device.decrypt_interleaved(ks, tu, tl, bu, ol2, st2)
+    device.decrypt_interleaved(ks, tu, tl, bu, ol2, st2, key_idx=kidx)
     torch.cuda.synchronize()
     assert int(st.abs().sum()) == 0 and bool((ol == L).all()) and torch.equal(back[:, :L], pt)
     assert torch.equal(st2, st) and torch.equal(ol2, ol) and torch.equal(device.deinterleave(bu, tl - 48), back)

@@ -17,8 +17,8 @@ def kernel_class(name):
     """encrypt / decrypt (the c2 kernels, as bench.py expects), or the kernel's
     own name for the others (long-token, verify, key setup, hkdf, ...)."""
     base = name.replace("(anonymous namespace)::", "").split("(")[0].split("<")[0].replace("rnstok::", "").replace("void ", "").strip()
-    if base in ("k_encrypt", "k_decrypt"):
-        return base[2:]
+    if base in ("k_encrypt", "k_decrypt", "k_encrypt_split"):
+        return base[2:].replace("_split", "")
     return base
 
 

@@ -353,7 +353,24 @@ constexpr uint32_t SPLIT_RING = LDS_ENC_BYTES;                    // 8 x 4 KiB
 constexpr uint32_t LDS_ENC_SPLIT_BYTES = SPLIT_RING + SPLIT_AES_WAVES * 4096u;
 static_assert(LDS_ENC_SPLIT_BYTES <= 160u * 1024u, "LDS");
 
-template <int NR, bool ILV = false, bool RB = ILV, bool PERKEY = false>
+// Wave maximum of a per-lane value (sorted chunks: lane 0 already holds it).
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)v, d, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+// GEN: packed batches (per-packet lengths and offsets, a length order and the
+// chunk counter of RT_F_SORT_BY_LENGTH), the shape of c5's encrypt half.  The
+// AES wave takes each 64-packet chunk (from the counter, or its static share)
+// and hands the chunk's first index to the hashing wave in the slot's lane-0
+// unit with the chunk's first quad; both run the chunk to its longest packet
+// (a length-ordered chunk is nearly uniform), each lane stopping at its own
+// last quad.  A chunk index past the batch tells the hashing wave to leave.
+template <int NR, bool ILV = false, bool RB = ILV, bool PERKEY = false, bool GEN = false>
 __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
     typedef __attribute__((address_space(3))) uint32_t lds_u32;
@@ -363,45 +380,78 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
     const uint32_t pair = aes ? wave : wave - SPLIT_AES_WAVES;
     const uint32_t slot = SPLIT_RING + 4096u * pair;
     lds_u32 *produced = (lds_u32 *)(uintptr_t)slot, *consumed = (lds_u32 *)(uintptr_t)(slot + 4u);
-    if (aes && lane < 2u) ((lds_u32 *)(uintptr_t)slot)[lane] = 0u;   // before the barrier
+    lds_u32 *chunk_at = (lds_u32 *)(uintptr_t)(slot + 8u);
+    if (aes && lane < 3u) ((lds_u32 *)(uintptr_t)slot)[lane] = 0u;   // before the barrier
     fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);     // ends with the workgroup barrier
 
-    const uint32_t L = a.uni_len, nfull = L >> 4, nq = nfull >> 2, tb = (nfull & 3u) + 1u, rem = L & 15u;
     const uint64_t US = ILV ? 16ull * a.n : 16ull;
     const uint32_t n_batches = (a.n + 63u) >> 6;
     const uint32_t first = blockIdx.x * SPLIT_AES_WAVES + pair, stride = gridDim.x * SPLIT_AES_WAVES;
     lds_q *mine = (lds_q *)(uintptr_t)(slot + 16u * lane);     // unit j at mine[64 j]
     const u32x4 z = {0u, 0u, 0u, 0u};
     uint32_t count = 0;                                    // quads handed over so far (both sides)
+    // packet i of the batch: plaintext / token offsets, length
+    auto pt_at = [&](uint32_t p) -> const uint8_t * {
+        return ILV ? a.pt + 16ull * p : a.pt + (GEN && a.pt_off ? a.pt_off[p] : (uint64_t)p * a.pt_stride);
+    };
+    auto tok_at = [&](uint32_t p) -> uint8_t * {
+        return ILV ? a.tok + 16ull * p : a.tok + (GEN && a.tok_off ? a.tok_off[p] : (uint64_t)p * a.tok_stride);
+    };
     if (aes) {
         const Lanes LN(threadIdx.x & 31u);
         Keys<NR, PERKEY> K;
         if (!PERKEY) K.load(a.rec, REC_ENC);
         Sha256 S;                                          // unused: enc_quad<NR, false> hashes nothing
-        for (uint32_t b = first; b < n_batches; b += stride) {
-            const uint32_t p = 64u * b + lane;
-            const bool valid = p < a.n;
-            if (PERKEY) K.load(a.rec + (uint64_t)a.key_idx[valid ? p : 0u] * REC_WORDS, REC_ENC);
-            const uint8_t *P = ILV ? a.pt + 16ull * p : a.pt + (uint64_t)p * a.pt_stride;
-            uint8_t *O = ILV ? a.tok + 16ull * p : a.tok + (uint64_t)p * a.tok_stride;
+        uint32_t b = first;
+        for (;;) {
+            uint64_t base;
+            if (GEN && a.queue) {
+                base = take_chunk(a.queue);
+            } else {
+                base = 64ull * b;
+                b += stride;
+            }
+            if (base >= a.n) {
+                if (GEN) {             // tell the hashing wave (it cannot know the counter's end)
+                    if (count)
+                        while (__hip_atomic_load(consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < count)
+                            __builtin_amdgcn_s_sleep(1);
+                    ++count;
+                    if (lane == 0u) {
+                        *chunk_at = 0xFFFFFFFFu;
+                        __hip_atomic_store(produced, count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                break;
+            }
+            const uint32_t i = (uint32_t)base + lane;
+            const bool valid = i < a.n;
+            const uint32_t p = valid ? (GEN && a.order ? a.order[i] : i) : 0u;
+            const uint32_t L = GEN && a.pt_len ? (valid ? a.pt_len[p] : 0u) : a.uni_len;
+            const uint32_t nfull = L >> 4, nq = nfull >> 2, tb = (nfull & 3u) + 1u, rem = L & 15u;
+            const uint32_t wq = GEN ? wave_max(valid ? nq : 0u) : nq;
+            if (PERKEY) K.load(a.rec + (uint64_t)a.key_idx[p] * REC_WORDS, REC_ENC);
+            const uint8_t *P = pt_at(p);
+            uint8_t *O = tok_at(p);
             u32x4 prev = valid ? ld16(a.iv + 16ull * p) : z;
             if (valid) st16(O, prev);
             uint8_t *C = O + US;
-            for (uint32_t q = 0; q <= nq; ++q) {
+            for (uint32_t q = 0; q <= wq; ++q) {
                 u32x4 x[4], c[4];
+                const bool act = valid && q <= nq;
                 if (q < nq) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) x[j] = valid ? ld16(P + US * j) : z;
                 } else {
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        x[j] = !valid ? z
-                                      : ((uint32_t)j + 1u < tb ? ld16(P + US * j)
-                                                               : ((uint32_t)j + 1u == tb ? pad_block(P + US * j, rem) : z));
+                        x[j] = !act ? z
+                                    : ((uint32_t)j + 1u < tb ? ld16(P + US * j)
+                                                             : ((uint32_t)j + 1u == tb ? pad_block(P + US * j, rem) : z));
                 }
                 enc_quad<NR, false>(c, x, prev, K.rk, LN, S);
                 const uint32_t nst = q < nq ? 4u : tb;
-                if (valid) {
+                if (act) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
                         if ((uint32_t)j < nst) st16(C + US * j, c[j]);
@@ -420,43 +470,66 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
                 ++count;
                 // lane 0's quad (read back from the token buffer) and the
                 // slot's writes before the count the hashing wave polls
-                if (lane == 0u) __hip_atomic_store(produced, count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (lane == 0u) {
+                    if (GEN && q == 0u) *chunk_at = (uint32_t)base;
+                    __hip_atomic_store(produced, count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
             }
         }
     } else {
-        for (uint32_t b = first; b < n_batches; b += stride) {
-            const uint32_t p = 64u * b + lane;
-            const bool valid = p < a.n;
-            uint8_t *O = ILV ? a.tok + 16ull * p : a.tok + (uint64_t)p * a.tok_stride;
+        uint32_t b = first;
+        for (;;) {
+            uint64_t base;
+            if (GEN) {
+                while (__hip_atomic_load(produced, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < count + 1u)
+                    __builtin_amdgcn_s_sleep(1);
+                const uint32_t c0 = __builtin_amdgcn_readfirstlane(*chunk_at);
+                if (c0 == 0xFFFFFFFFu) break;
+                base = c0;
+            } else {
+                if (b >= n_batches) break;
+                base = 64ull * b;
+                b += stride;
+            }
+            const uint32_t i = (uint32_t)base + lane;
+            const bool valid = i < a.n;
+            const uint32_t p = valid ? (GEN && a.order ? a.order[i] : i) : 0u;
+            const uint32_t L = GEN && a.pt_len ? (valid ? a.pt_len[p] : 0u) : a.uni_len;
+            const uint32_t nfull = L >> 4, nq = nfull >> 2, tb = (nfull & 3u) + 1u;
+            const uint32_t wq = GEN ? wave_max(valid ? nq : 0u) : nq;
+            uint8_t *O = tok_at(p);
             const uint8_t *C = O + US;
             uint32_t h[8];
-            const uint32_t *r = PERKEY ? a.rec + (uint64_t)a.key_idx[valid ? p : 0u] * REC_WORDS : a.rec;
+            const uint32_t *r = PERKEY ? a.rec + (uint64_t)a.key_idx[p] * REC_WORDS : a.rec;
             if (PERKEY)
                 load8(h, r + REC_IPAD);
             else
                 load_uniform8(h, a.rec + REC_IPAD);
             u32x4 up = valid ? ld16(a.iv + 16ull * p) : z;      // the unit before the quad (IV first)
             uint32_t w[16];
-            for (uint32_t q = 0; q <= nq; ++q) {
+            for (uint32_t q = 0; q <= wq; ++q) {
                 while (__hip_atomic_load(produced, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < count + 1u)
                     __builtin_amdgcn_s_sleep(1);
                 const uint32_t nst = q < nq ? 4u : tb;
+                const bool act = valid && q <= nq;
                 u32x4 c[4];
                 if (!RB && lane) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) c[j] = mine[64 * j];
                 } else {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) c[j] = (valid && (uint32_t)j < nst) ? ld16(C + US * j) : z;
+                    for (int j = 0; j < 4; ++j) c[j] = (act && (uint32_t)j < nst) ? ld16(C + US * j) : z;
                 }
                 ++count;
                 // the slot's reads complete before the AES wave may overwrite it
                 if (!RB && lane == 0u)
                     __hip_atomic_store(consumed, count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 C += 4 * US;
-                sha_units(w, up, c[0], c[1], c[2]);
-                if (q < nq) sha256_compress(h, w);
-                up = c[3];
+                if (!GEN || q <= nq) {
+                    sha_units(w, up, c[0], c[1], c[2]);
+                    if (q < nq) sha256_compress(h, w);
+                    up = c[3];
+                }
             }
             // w: units u0..u3 of the tail quad, up = u4 (units past the
             // packet's own are not hashed); tu = tb + 1 units are left for the
@@ -1532,8 +1605,12 @@ static Shape shape_for(uint32_t n, int max_threads, int n_cu) {
 #ifndef RNSTOK_SPLIT_PERKEY          // per-packet keys (c3) on the split kernel too: 0.845 vs 0.912 ms rows,
 #define RNSTOK_SPLIT_PERKEY 1        // 0.770 vs 0.852 interleaved (profiles/r04_split/r04i_perkey_ab.txt)
 #endif
+#ifndef RNSTOK_SPLIT_GEN             // packed / length-ordered batches (c5) on the split kernel too
+#define RNSTOK_SPLIT_GEN 1
+#endif
 static bool use_split_enc(const EncArgs &a, int n_cu) {
-    return RNSTOK_SPLIT_ENC && (!a.key_idx || RNSTOK_SPLIT_PERKEY) && !a.pt_len && !a.order && !a.queue &&
+    const bool gen = a.pt_len || a.order || a.queue || a.pt_off;
+    return RNSTOK_SPLIT_ENC && (!a.key_idx || RNSTOK_SPLIT_PERKEY) && (!gen || RNSTOK_SPLIT_GEN) &&
            (uint64_t)a.n >= 64ull * SPLIT_AES_WAVES * (uint64_t)n_cu;
 }
 static uint64_t split_grid(uint32_t n, int n_cu) {
@@ -1544,17 +1621,22 @@ static uint64_t split_grid(uint32_t n, int n_cu) {
 template <int NR>
 static hipError_t launch_enc_split_nr(const EncArgs &a, int n_cu, hipStream_t s) {
     const uint64_t grid = split_grid(a.n, n_cu);
-#define RT_SPLIT(ILV_, RB_, PK_)                                                                            \
-    hipLaunchKernelGGL((k_encrypt_split<NR, ILV_, RB_, PK_>), dim3((unsigned)grid), dim3(SPLIT_THREADS), \
+#define RT_SPLIT(ILV_, RB_, PK_, GEN_)                                                                        \
+    hipLaunchKernelGGL((k_encrypt_split<NR, ILV_, RB_, PK_, GEN_>), dim3((unsigned)grid), dim3(SPLIT_THREADS), \
                        LDS_ENC_SPLIT_BYTES, s, a)
-    if (a.ilv && a.key_idx)
-        RT_SPLIT(true, RNSTOK_SPLIT_ILV_RB, true);
+    const bool gen = a.pt_len || a.order || a.queue || a.pt_off;
+    if (gen && a.key_idx)
+        RT_SPLIT(false, false, true, true);
+    else if (gen)
+        RT_SPLIT(false, false, false, true);
+    else if (a.ilv && a.key_idx)
+        RT_SPLIT(true, RNSTOK_SPLIT_ILV_RB, true, false);
     else if (a.ilv)
-        RT_SPLIT(true, RNSTOK_SPLIT_ILV_RB, false);
+        RT_SPLIT(true, RNSTOK_SPLIT_ILV_RB, false, false);
     else if (a.key_idx)
-        RT_SPLIT(false, RNSTOK_SPLIT_ROWS_RB, true);
+        RT_SPLIT(false, RNSTOK_SPLIT_ROWS_RB, true, false);
     else
-        RT_SPLIT(false, RNSTOK_SPLIT_ROWS_RB, false);
+        RT_SPLIT(false, RNSTOK_SPLIT_ROWS_RB, false, false);
 #undef RT_SPLIT
     return hipGetLastError();
 }
@@ -1755,6 +1837,10 @@ hipError_t configure_kernels() {
     RT_CFG((k_decrypt<10, false, WG_DEC, true>), LDS_DEC_BYTES);
     RT_CFG((k_decrypt<10, false, 1024, true>), LDS_DEC_BYTES);
     RT_CFG((k_decrypt<10, true, WG_PERKEY_DEC, true>), LDS_DEC_BYTES);
+    RT_CFG((k_encrypt_split<14, false, false, false, true>), LDS_ENC_SPLIT_BYTES);
+    RT_CFG((k_encrypt_split<14, false, false, true, true>), LDS_ENC_SPLIT_BYTES);
+    RT_CFG((k_encrypt_split<10, false, false, false, true>), LDS_ENC_SPLIT_BYTES);
+    RT_CFG((k_encrypt_split<10, false, false, true, true>), LDS_ENC_SPLIT_BYTES);
     RT_CFG((k_encrypt_split<14, false, RNSTOK_SPLIT_ROWS_RB, false>), LDS_ENC_SPLIT_BYTES);
     RT_CFG((k_encrypt_split<14, true, RNSTOK_SPLIT_ILV_RB, false>), LDS_ENC_SPLIT_BYTES);
     RT_CFG((k_encrypt_split<10, false, RNSTOK_SPLIT_ROWS_RB, false>), LDS_ENC_SPLIT_BYTES);

@@ -135,3 +135,46 @@ def test_split_decrypt_failures_match_the_oracle(rt, layout):
     ok = st_h == 0
     assert (ol_h[ok] == L).all()
     assert np.array_equal(back[ok, :L], pt.cpu().numpy()[ok])
+
+
+@pytest.mark.parametrize("sort,n_keys,lo,hi", [(True, 97, 0, 700), (False, 1, 0, 300), (True, 1, 64, 4096),
+                                              (False, 65536, 500, 520)])
+def test_split_kernel_packed_batches(rt, sort, n_keys, lo, hi):
+    """Packed batches (per-packet lengths and offsets, c5's shape) at split
+    sizes, length-ordered (the chunk counter) or not: every token against the
+    oracle on a sample, every packet round-tripped."""
+    import torch
+    from reticulum_amd import device
+    n = _split_n(77)
+    rng = np.random.Generator(np.random.PCG64(77 + n_keys + lo))
+    keys = rng.integers(0, 256, (n_keys, 64), dtype=np.uint8)
+    ks = rt.KeySet(keys if n_keys > 1 else keys[0].tobytes())
+    lens = rng.integers(lo, hi + 1, n).astype(np.int32)
+    off = np.zeros(n, np.int64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.int64))
+    tl = (16 + 16 * (lens // 16 + 1) + 32).astype(np.int64)
+    toff = np.zeros(n, np.int64)
+    toff[1:] = np.cumsum(tl[:-1])
+    g = torch.Generator(device="cuda").manual_seed(int(lo) + 3)
+    pt = torch.randint(0, 256, (int(lens.sum()) + 1,), dtype=torch.uint8, device="cuda", generator=g)
+    iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
+    kidx = torch.from_numpy(rng.integers(0, n_keys, n).astype(np.int32)).cuda() if n_keys > 1 else None
+    d = lambda a: torch.from_numpy(a).cuda()     # noqa: E731
+    tok = torch.full((int(tl.sum()),), 0xEE, dtype=torch.uint8, device="cuda")
+    device.encrypt(ks, pt, d(off), d(lens), iv, tok, d(toff), key_idx=kidx, sort=sort)
+    poff = np.zeros(n, np.int64)
+    poff[1:] = np.cumsum((tl - 48)[:-1])
+    back = torch.zeros(int((tl - 48).sum()), dtype=torch.uint8, device="cuda")
+    ol = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    device.decrypt(ks, tok, d(toff), d(tl.astype(np.int32)), back, d(poff), ol, st, key_idx=kidx, sort=sort)
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0 and np.array_equal(ol.cpu().numpy(), lens)
+    t_h, p_h, b_h, iv_h = tok.cpu().numpy(), pt.cpu().numpy(), back.cpu().numpy(), iv.cpu().numpy()
+    kx = kidx.cpu().numpy() if kidx is not None else np.zeros(n, np.int64)
+    for i in range(n):
+        assert b_h[poff[i]:poff[i] + lens[i]].tobytes() == p_h[off[i]:off[i] + lens[i]].tobytes(), i
+    sel = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, 60)]))
+    for i in sel:
+        want = oracle.encrypt(keys[kx[i]].tobytes(), iv_h[i].tobytes(), p_h[off[i]:off[i] + lens[i]].tobytes())
+        assert t_h[toff[i]:toff[i] + tl[i]].tobytes() == want, i

@@ -362,7 +362,7 @@ def main():
     # once on its own shard, over its own PCIe link (the node's host-origin rate)
     # (N > 1: below, after the headline line exists, under a deadline)
     e2e = e2e_rate(ks, pt, iv, L, tl, n, stream) if args.e2e and world == 1 else None
-    node = shard8 = c5share = None
+    node = shard8 = c5share = c3leg = None
     if args.node and world == 1 and args.config == "c2":
         try:
             node = node_rate(dev)
@@ -380,6 +380,10 @@ def main():
             c5share = c5_share_rate(dev, _native.load().rt_num_cus(_native.context(local)))
         except Exception as exc:
             c5share = {"error": f"{type(exc).__name__}: {exc}"}
+        try:
+            c3leg = c3_rate(dev, _native.load().rt_num_cus(_native.context(local)))
+        except Exception as exc:
+            c3leg = {"error": f"{type(exc).__name__}: {exc}"}
 
     lib = _native.load()
     n_cu = lib.rt_num_cus(_native.context(local))
@@ -479,6 +483,7 @@ def main():
         "node_pipeline": node,
         "c4_rank_share_8gpu": shard8,
         "c5_rank_share_8gpu": c5share,
+        "c3_per_key": c3leg,
         "sharded_c4": None,
     }
 
@@ -842,6 +847,27 @@ def sharded_bench(cfg, args, world, rank, local, reps=3):
         total["pipelined_s"] = total.get("pipelined_s", 0.0) + (piped_s or 0.0)
     pkts = n
     byts_all = int(lens.to(torch.int64).sum())
+    # canonical ops of the compute phases over the real lengths (SURVEY
+    # §8(d)), priced against every rank's VALU peak; the time is the
+    # host-timed compute phase (max over ranks: bucketing, allocation and
+    # launches included), so this frac is a lower bound of the kernels'
+    L64 = lens.to(torch.int64)
+    B = L64 // 16 + 1
+    ops = AES_BLOCK_OPS * B + SHA_CMP_OPS * ((64 + 16 + 16 * B + 9 + 63) // 64)
+    if cfg == "c4":
+        ops_all = 2 * int(ops.sum()) + TAG_CMP_OPS * n
+    else:
+        ops_all = int(ops.sum()) + TAG_CMP_OPS * (n - h)
+    from reticulum_amd import _native
+    n_cu = _native.load().rt_num_cus(_native.context(local))
+    peak = world * n_cu * 128 * 2.4e9
+    report["roofline"] = {"bound": "valu", "kernel": "compute phases (every rank's bucketing passes and kernels)",
+                          "achieved": ops_all / total["compute_s"] / 1e12, "peak": peak / 1e12, "unit": "TOP/s",
+                          "frac": ops_all / total["compute_s"] / peak, "traffic": None,
+                          "note": "canonical int32 VALU lane-ops (352/AES block, 1464/SHA-256 compression, +8 per "
+                                  "tag compare) summed over the real lengths / host-timed compute phases (max over "
+                                  "ranks) / (ranks x CUs x 128 x 2.4 GHz): a lower bound of the kernels' fraction; "
+                                  "per-kernel HBM traffic of these shapes: profiles/r04m_c5, profiles/r04j_pmc.json"}
     report.update({
         "value": pkts / total["compute_s"],
         "unit": ("round trips/s (device-resident, all ranks, compute phases: every segment encrypted, then its "
@@ -1308,6 +1334,50 @@ def c5_share_rate(dev, n_cu, n=1 << 20, steps=10, n_keys=65536):
     res["note"] = ("one rank's share of c5 at 8 GPUs; per direction the length-bucketing passes (histogram, scan, "
                    "scatter) and the per-key kernel are timed together; frac = canonical ops summed over the real "
                    "lengths / time / (CUs x 128 x 2.4 GHz)")
+    return res
+
+
+def c3_rate(dev, n_cu, n=1 << 20, L=500, n_keys=65536, steps=10):
+    """SURVEY §8(d) c3 beside the headline: the c2 batch (2^20 x 500 B, packed
+    rows) with a per-packet key index into a 65 536-key table (Token objects
+    of many links), through the product's uniform entry points.  Median of
+    ``steps`` HIP-event timings per direction after the clock warmup; every
+    status and length checked and the plaintexts compared (round trip)."""
+    import torch
+    import reticulum_amd as rt
+    from reticulum_amd import device
+    g = torch.Generator(device=dev).manual_seed(33)
+    kg = torch.Generator().manual_seed(333)
+    keys = torch.randint(0, 256, (n_keys, 64), dtype=torch.uint8, generator=kg).numpy()
+    ks = rt.KeySet(keys, device=dev.index if dev.index is not None else 0)
+    tl = rt.token_len(L)
+    kidx = torch.randint(0, n_keys, (n,), dtype=torch.int32, device=dev, generator=g)
+    pt = torch.randint(0, 256, (n, L), dtype=torch.uint8, device=dev, generator=g)
+    iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
+    tok = torch.empty((n, tl), dtype=torch.uint8, device=dev)
+    back = torch.empty((n, tl - 48), dtype=torch.uint8, device=dev)
+    ol = torch.empty(n, dtype=torch.int32, device=dev)
+    st = torch.empty(n, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    enc = lambda: device.encrypt_uniform(ks, pt, L, iv, tok, key_idx=kidx, stream=stream)            # noqa: E731
+    dec = lambda: device.decrypt_uniform(ks, tok, tl, back, ol, st, key_idx=kidx, stream=stream)     # noqa: E731
+    peak = n_cu * 128 * 2.4e9
+    res = {"packets": n, "plaintext_bytes": L, "keys": n_keys, "layout": "packed rows"}
+    for name, f, o in (("encrypt", enc, ops_enc(L) * n), ("decrypt", dec, ops_dec(L) * n)):
+        warmup(f, stream, 2, 0.3)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for a, b in ev:
+            a.record(stream)
+            f()
+            b.record(stream)
+        torch.cuda.synchronize()
+        ms = sorted(a.elapsed_time(b) for a, b in ev)[steps // 2]
+        res[name] = {"ms": ms, "packets_s": n / (ms * 1e-3), "frac_of_valu_peak": o / (ms * 1e-3) / peak}
+    res["ok"] = bool((st == 0).all()) and bool((ol == L).all()) and torch.equal(back[:, :L], pt)
+    res["round_trips_s"] = n / ((res["encrypt"]["ms"] + res["decrypt"]["ms"]) * 1e-3)
+    res["note"] = ("c3 (SURVEY §8(d)): the c2 batch with per-packet keys (key_idx into a 65 536-key table), "
+                   "kernel time per direction (HIP events, median); key setup is timed apart under key_setup "
+                   "when bench runs --config c3")
     return res
 
 

@@ -22,6 +22,18 @@
 namespace rnstok {
 
 // Workgroup sizes: one workgroup per CU (the LDS table image is 128/160 KiB).
+// Packed rows: 16-B units at a 560-B row stride share 128-B lines between
+// consecutive quads, and one quad apart the line has left L2 (profiles/r04o,
+// r04p, r04q, one-process A/Bs at c2 / 1500 B / packed):
+#ifndef RNSTOK_ENC_PAIR              // split encrypt, plaintext quads loaded in pairs: fetch -13 %, time -0.5 %
+#define RNSTOK_ENC_PAIR 1
+#endif
+#ifndef RNSTOK_ENC_STPAIR            // split encrypt, token quads stored in pairs: writes -22 %, time +2.2 %
+#define RNSTOK_ENC_STPAIR 0          // (not adopted)
+#endif
+#ifndef RNSTOK_DEC_PAIR              // decrypt, one key, token quads loaded in pairs: fetch -21 %, time -1.6 %
+#define RNSTOK_DEC_PAIR 1
+#endif
 #ifndef RNSTOK_WG_ENC
 #define RNSTOK_WG_ENC 1024      // single key: 4 waves/SIMD, 128 VGPRs
 #endif
@@ -436,12 +448,22 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
             u32x4 prev = valid ? ld16(a.iv + 16ull * p) : z;
             if (valid) st16(O, prev);
             uint8_t *C = O + US;
+            // packed rows: full quads loaded in line-sharing pairs (k_decrypt)
+            constexpr bool PAIR = RNSTOK_ENC_PAIR && !ILV;
+            u32x4 nx[4], held[4];
             for (uint32_t q = 0; q <= wq; ++q) {
                 u32x4 x[4], c[4];
                 const bool act = valid && q <= nq;
-                if (q < nq) {
+                if (PAIR && (q & 1u) && q < nq) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) x[j] = nx[j];
+                } else if (q < nq) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) x[j] = valid ? ld16(P + US * j) : z;
+                    if (PAIR && q + 1u < nq) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) nx[j] = valid ? ld16(P + US * (4 + j)) : z;
+                    }
                 } else {
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
@@ -451,10 +473,23 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
                 }
                 enc_quad<NR, false>(c, x, prev, K.rk, LN, S);
                 const uint32_t nst = q < nq ? 4u : tb;
+                // packed rows: an even full quad's ciphertext is stored with
+                // the next quad's (the 128 B written while their lines sit in
+                // L2), except lane 0's, which its hashing wave reads back now
+                constexpr bool STPAIR = RNSTOK_ENC_STPAIR && !ILV && !RB && !PERKEY;
                 if (act) {
+                    if (STPAIR && lane && !(q & 1u) && q < nq) {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        if ((uint32_t)j < nst) st16(C + US * j, c[j]);
+                        for (int j = 0; j < 4; ++j) held[j] = c[j];
+                    } else {
+                        if (STPAIR && lane && (q & 1u)) {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) st16(C - 4 * US + US * j, held[j]);
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if ((uint32_t)j < nst) st16(C + US * j, c[j]);
+                    }
                 }
                 prev = c[3];
                 P += 4 * US;
@@ -887,6 +922,7 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
 
 // --------------------------------------------------------------- decrypt --
 
+
 // WG: the workgroup size the kernel is compiled for (its VGPR budget).  One
 // key: 768 threads (168 VGPRs) for batches of several passes, 1024 (128
 // VGPRs, 4 waves/SIMD) when one pass covers the batch (e.g. 16 KiB Resource
@@ -956,13 +992,31 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
             uint8_t *D = O;
             Sha256 S;
             u32x4 c[4], pp[4];
+            // packed rows: an even quad loads the next quad's 64 B with its
+            // own, so the 128-B line the two share is read while it is in
+            // L2 (one quad apart, an XCD's waves have streamed more than its
+            // L2 through and the line is fetched again: 2.7x read traffic)
+            constexpr bool PAIR = RNSTOK_DEC_PAIR && !ILV && !PERKEY;
+            u32x4 nx[4];
 #pragma nounroll
             for (uint32_t q = 0; q <= nq; ++q) {
                 const uint32_t nbk = q < nq ? 4u : tb;
-                c[0] = ld16(C);
-                c[1] = nbk > 1u ? ld16(C + US) : z;
-                c[2] = nbk > 2u ? ld16(C + 2 * US) : z;
-                c[3] = nbk > 3u ? ld16(C + 3 * US) : z;
+                if (PAIR && (q & 1u)) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) c[k] = nx[k];
+                } else {
+                    c[0] = ld16(C);
+                    c[1] = nbk > 1u ? ld16(C + US) : z;
+                    c[2] = nbk > 2u ? ld16(C + 2 * US) : z;
+                    c[3] = nbk > 3u ? ld16(C + 3 * US) : z;
+                    if (PAIR && q < nq) {
+                        const uint32_t nb1 = q + 1u < nq ? 4u : tb;
+                        nx[0] = ld16(C + 4 * US);
+                        nx[1] = nb1 > 1u ? ld16(C + 5 * US) : z;
+                        nx[2] = nb1 > 2u ? ld16(C + 6 * US) : z;
+                        nx[3] = nb1 > 3u ? ld16(C + 7 * US) : z;
+                    }
+                }
                 S.start(h);
                 sha_units(S.w, prev, c[0], c[1], c[2]);
                 dec_quad<NR, true>(pp, c, prev, K.rk, LN, S);

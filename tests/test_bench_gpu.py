@@ -23,6 +23,7 @@ def test_sharded_config_world1(cfg, packets):
     assert rep["phases"]["encrypt"]["packets"] == per
     assert rep["phases"]["decrypt"]["packets"] == packets - (0 if cfg == "c4" else per)
     assert rep["value"] > 0 and rep["compute_ms"] > 0
+    assert rep["roofline"]["bound"] == "valu" and 0 < rep["roofline"]["frac"] < 1
 
 
 def test_c3_key_setup_times():
@@ -54,3 +55,13 @@ def test_shard_rate_small():
     r = bench.shard_rate(torch.device("cuda", 0), 8, steps=3, L=4096, per_cu=16)
     assert r["ok"] is True and r["tokens"] == 128
     assert r["encrypt"]["ms"] > 0 and r["decrypt"]["ms"] > 0 and 0 < r["encrypt"]["frac_of_valu_peak"] < 1
+
+
+def test_c3_rate_small():
+    """bench.c3_rate (the per-key c3 leg of the bench line) at a small size:
+    both directions timed, every packet back."""
+    import torch
+    import bench
+    r = bench.c3_rate(torch.device("cuda", 0), 8, n=8192, n_keys=97, steps=3)
+    assert r["ok"] is True and r["packets"] == 8192
+    assert r["encrypt"]["ms"] > 0 and r["decrypt"]["ms"] > 0 and r["round_trips_s"] > 0

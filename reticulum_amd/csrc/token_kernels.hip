@@ -28,8 +28,9 @@ namespace rnstok {
 #ifndef RNSTOK_ENC_PAIR              // split encrypt, plaintext quads loaded in pairs: fetch -13 %, time -0.5 %
 #define RNSTOK_ENC_PAIR 1
 #endif
-#ifndef RNSTOK_ENC_STPAIR            // split encrypt, token quads stored in pairs: writes -22 %, time +2.2 %
-#define RNSTOK_ENC_STPAIR 0          // (not adopted)
+// (split encrypt, token quads stored in pairs: writes -22 %, time +2.2 %: not adopted, r04q)
+#ifndef RNSTOK_SPLIT_NOWAIT          // split encrypt, packed rows: AES waves never wait for the slot
+#define RNSTOK_SPLIT_NOWAIT 0
 #endif
 #ifndef RNSTOK_DEC_PAIR              // decrypt, one key, token quads loaded in pairs: fetch -21 %, time -1.6 %
 #define RNSTOK_DEC_PAIR 1
@@ -382,6 +383,14 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 // unit with the chunk's first quad; both run the chunk to its longest packet
 // (a length-ordered chunk is nearly uniform), each lane stopping at its own
 // last quad.  A chunk index past the batch tells the hashing wave to leave.
+#ifdef RNSTOK_SPLIT_PROBE
+// timing probe (probe builds only): per role, cycles spent waiting on the
+// other role, waits entered, cycles from the table fill to the end
+__device__ unsigned long long g_split_probe[8];
+#define SPLIT_PROBE(x) x
+#else
+#define SPLIT_PROBE(x)
+#endif
 template <int NR, bool ILV = false, bool RB = ILV, bool PERKEY = false, bool GEN = false>
 __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
@@ -393,8 +402,15 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
     const uint32_t slot = SPLIT_RING + 4096u * pair;
     lds_u32 *produced = (lds_u32 *)(uintptr_t)slot, *consumed = (lds_u32 *)(uintptr_t)(slot + 4u);
     lds_u32 *chunk_at = (lds_u32 *)(uintptr_t)(slot + 8u);
-    if (aes && lane < 3u) ((lds_u32 *)(uintptr_t)slot)[lane] = 0u;   // before the barrier
+    lds_u32 *ring_at = (lds_u32 *)(uintptr_t)(slot + 12u);   // count of the quad in the slot (NOWAIT)
+    if (aes && lane < 4u) ((lds_u32 *)(uintptr_t)slot)[lane] = 0u;   // before the barrier
+    // NOWAIT (packed rows, uniform batches): the AES wave never waits for
+    // the slot; a quad that finds it still taken goes to the hashing wave
+    // through the token buffer only (read back), the others through LDS
+    constexpr bool NOWAIT = RNSTOK_SPLIT_NOWAIT && !RB && !GEN;
+    uint32_t last_ring = 0;                                // AES side: count of the last quad put in the slot
     fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);     // ends with the workgroup barrier
+    SPLIT_PROBE(uint64_t pr_wait = 0; uint64_t pr_n = 0; const uint64_t pr_t0 = clock64();)
 
     const uint64_t US = ILV ? 16ull * a.n : 16ull;
     const uint32_t n_batches = (a.n + 63u) >> 6;
@@ -450,7 +466,7 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
             uint8_t *C = O + US;
             // packed rows: full quads loaded in line-sharing pairs (k_decrypt)
             constexpr bool PAIR = RNSTOK_ENC_PAIR && !ILV;
-            u32x4 nx[4], held[4];
+            u32x4 nx[4];
             for (uint32_t q = 0; q <= wq; ++q) {
                 u32x4 x[4], c[4];
                 const bool act = valid && q <= nq;
@@ -473,40 +489,38 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
                 }
                 enc_quad<NR, false>(c, x, prev, K.rk, LN, S);
                 const uint32_t nst = q < nq ? 4u : tb;
-                // packed rows: an even full quad's ciphertext is stored with
-                // the next quad's (the 128 B written while their lines sit in
-                // L2), except lane 0's, which its hashing wave reads back now
-                constexpr bool STPAIR = RNSTOK_ENC_STPAIR && !ILV && !RB && !PERKEY;
                 if (act) {
-                    if (STPAIR && lane && !(q & 1u) && q < nq) {
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) held[j] = c[j];
-                    } else {
-                        if (STPAIR && lane && (q & 1u)) {
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) st16(C - 4 * US + US * j, held[j]);
-                        }
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if ((uint32_t)j < nst) st16(C + US * j, c[j]);
-                    }
+                    for (int j = 0; j < 4; ++j)
+                        if ((uint32_t)j < nst) st16(C + US * j, c[j]);
                 }
                 prev = c[3];
                 P += 4 * US;
                 C += 4 * US;
                 // the slot is free once the hashing wave has taken every earlier quad
-                if (!RB && count)
-                    while (__hip_atomic_load(consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < count)
+                bool to_ring = !RB;
+                if (NOWAIT) {
+                    to_ring = __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                  consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) >= last_ring;
+                } else if (!RB && count) {
+                    SPLIT_PROBE(const uint64_t pw = clock64(); bool pwt = false;)
+                    while (__hip_atomic_load(consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < count) {
+                        SPLIT_PROBE(pwt = true;)
                         __builtin_amdgcn_s_sleep(1);
-                if (!RB && lane) {
+                    }
+                    SPLIT_PROBE(if (pwt) { pr_wait += clock64() - pw; ++pr_n; })
+                }
+                if (to_ring && lane) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) mine[64 * j] = c[j];
                 }
                 ++count;
+                if (NOWAIT && to_ring) last_ring = count;
                 // lane 0's quad (read back from the token buffer) and the
                 // slot's writes before the count the hashing wave polls
                 if (lane == 0u) {
                     if (GEN && q == 0u) *chunk_at = (uint32_t)base;
+                    if (NOWAIT && to_ring) __hip_atomic_store(ring_at, count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     __hip_atomic_store(produced, count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
@@ -543,12 +557,20 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
             u32x4 up = valid ? ld16(a.iv + 16ull * p) : z;      // the unit before the quad (IV first)
             uint32_t w[16];
             for (uint32_t q = 0; q <= wq; ++q) {
-                while (__hip_atomic_load(produced, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < count + 1u)
+                SPLIT_PROBE(const uint64_t pw = clock64(); bool pwt = false;)
+                while (__hip_atomic_load(produced, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < count + 1u) {
+                    SPLIT_PROBE(pwt = true;)
                     __builtin_amdgcn_s_sleep(1);
+                }
+                SPLIT_PROBE(if (pwt) { pr_wait += clock64() - pw; ++pr_n; })
                 const uint32_t nst = q < nq ? 4u : tb;
                 const bool act = valid && q <= nq;
                 u32x4 c[4];
-                if (!RB && lane) {
+                // NOWAIT: the quad is in the slot only if the slot's count is its own
+                const bool from_ring =
+                    !RB && (!NOWAIT || __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                           ring_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == count + 1u);
+                if (from_ring && lane) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) c[j] = mine[64 * j];
                 } else {
@@ -587,6 +609,15 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
             }
         }
     }
+#ifdef RNSTOK_SPLIT_PROBE
+    if (lane == 0u) {
+        const uint32_t r = aes ? 0u : 1u;
+        atomicAdd(&g_split_probe[r], pr_wait);
+        atomicAdd(&g_split_probe[2 + r], pr_n);
+        atomicAdd(&g_split_probe[4 + r], clock64() - pr_t0);
+        atomicAdd(&g_split_probe[6 + r], 1ull);
+    }
+#endif
 }
 
 // ---------------------------------------------------- encrypt, long tokens --
@@ -1908,3 +1939,13 @@ hipError_t configure_kernels() {
 }
 
 }  // namespace rnstok
+
+#ifdef RNSTOK_SPLIT_PROBE
+// probe builds only: read and clear k_encrypt_split's wait counters
+extern "C" int rt_split_probe_read(unsigned long long *out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rnstok::g_split_probe), sizeof(unsigned long long) * 8) != hipSuccess)
+        return -1;
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(rnstok::g_split_probe), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -29,9 +29,6 @@ namespace rnstok {
 #define RNSTOK_ENC_PAIR 1
 #endif
 // (split encrypt, token quads stored in pairs: writes -22 %, time +2.2 %: not adopted, r04q)
-#ifndef RNSTOK_SPLIT_NOWAIT          // split encrypt, packed rows: AES waves never wait for the slot
-#define RNSTOK_SPLIT_NOWAIT 0
-#endif
 #ifndef RNSTOK_DEC_PAIR              // decrypt, one key, token quads loaded in pairs: fetch -21 %, time -1.6 %
 #define RNSTOK_DEC_PAIR 1
 #endif
@@ -402,13 +399,7 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
     const uint32_t slot = SPLIT_RING + 4096u * pair;
     lds_u32 *produced = (lds_u32 *)(uintptr_t)slot, *consumed = (lds_u32 *)(uintptr_t)(slot + 4u);
     lds_u32 *chunk_at = (lds_u32 *)(uintptr_t)(slot + 8u);
-    lds_u32 *ring_at = (lds_u32 *)(uintptr_t)(slot + 12u);   // count of the quad in the slot (NOWAIT)
-    if (aes && lane < 4u) ((lds_u32 *)(uintptr_t)slot)[lane] = 0u;   // before the barrier
-    // NOWAIT (packed rows, uniform batches): the AES wave never waits for
-    // the slot; a quad that finds it still taken goes to the hashing wave
-    // through the token buffer only (read back), the others through LDS
-    constexpr bool NOWAIT = RNSTOK_SPLIT_NOWAIT && !RB && !GEN;
-    uint32_t last_ring = 0;                                // AES side: count of the last quad put in the slot
+    if (aes && lane < 3u) ((lds_u32 *)(uintptr_t)slot)[lane] = 0u;   // before the barrier
     fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);     // ends with the workgroup barrier
     SPLIT_PROBE(uint64_t pr_wait = 0; uint64_t pr_n = 0; const uint64_t pr_t0 = clock64();)
 
@@ -498,11 +489,7 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
                 P += 4 * US;
                 C += 4 * US;
                 // the slot is free once the hashing wave has taken every earlier quad
-                bool to_ring = !RB;
-                if (NOWAIT) {
-                    to_ring = __builtin_amdgcn_readfirstlane(__hip_atomic_load(
-                                  consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) >= last_ring;
-                } else if (!RB && count) {
+                if (!RB && count) {
                     SPLIT_PROBE(const uint64_t pw = clock64(); bool pwt = false;)
                     while (__hip_atomic_load(consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < count) {
                         SPLIT_PROBE(pwt = true;)
@@ -510,17 +497,15 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
                     }
                     SPLIT_PROBE(if (pwt) { pr_wait += clock64() - pw; ++pr_n; })
                 }
-                if (to_ring && lane) {
+                if (!RB && lane) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) mine[64 * j] = c[j];
                 }
                 ++count;
-                if (NOWAIT && to_ring) last_ring = count;
                 // lane 0's quad (read back from the token buffer) and the
                 // slot's writes before the count the hashing wave polls
                 if (lane == 0u) {
                     if (GEN && q == 0u) *chunk_at = (uint32_t)base;
-                    if (NOWAIT && to_ring) __hip_atomic_store(ring_at, count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     __hip_atomic_store(produced, count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
@@ -566,11 +551,7 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
                 const uint32_t nst = q < nq ? 4u : tb;
                 const bool act = valid && q <= nq;
                 u32x4 c[4];
-                // NOWAIT: the quad is in the slot only if the slot's count is its own
-                const bool from_ring =
-                    !RB && (!NOWAIT || __builtin_amdgcn_readfirstlane(__hip_atomic_load(
-                                           ring_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == count + 1u);
-                if (from_ring && lane) {
+                if (!RB && lane) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) c[j] = mine[64 * j];
                 } else {

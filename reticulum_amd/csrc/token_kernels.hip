@@ -29,6 +29,9 @@ namespace rnstok {
 #define RNSTOK_ENC_PAIR 1
 #endif
 // (split encrypt, token quads stored in pairs: writes -22 %, time +2.2 %: not adopted, r04q)
+#ifndef RNSTOK_SPLIT_TILE            // experiment: packed split encrypt reads 64-packet plaintext tiles
+#define RNSTOK_SPLIT_TILE 0
+#endif
 #ifndef RNSTOK_DEC_PAIR              // decrypt, one key, token quads loaded in pairs: fetch -21 %, time -1.6 %
 #define RNSTOK_DEC_PAIR 1
 #endif
@@ -455,6 +458,10 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
             u32x4 prev = valid ? ld16(a.iv + 16ull * p) : z;
             if (valid) st16(O, prev);
             uint8_t *C = O + US;
+            // (experiment, RNSTOK_SPLIT_TILE: packed batches whose plaintexts a
+            // gather pass laid out as 64-packet tiles, unit u of lane l at
+            // pt_off + 1024 u; tokens stay byte strings)
+            const uint64_t USP = GEN && RNSTOK_SPLIT_TILE ? 1024ull : US;
             // packed rows: full quads loaded in line-sharing pairs (k_decrypt)
             constexpr bool PAIR = RNSTOK_ENC_PAIR && !ILV;
             u32x4 nx[4];
@@ -466,17 +473,17 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
                     for (int j = 0; j < 4; ++j) x[j] = nx[j];
                 } else if (q < nq) {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) x[j] = valid ? ld16(P + US * j) : z;
+                    for (int j = 0; j < 4; ++j) x[j] = valid ? ld16(P + USP * j) : z;
                     if (PAIR && q + 1u < nq) {
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) nx[j] = valid ? ld16(P + US * (4 + j)) : z;
+                        for (int j = 0; j < 4; ++j) nx[j] = valid ? ld16(P + USP * (4 + j)) : z;
                     }
                 } else {
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
                         x[j] = !act ? z
-                                    : ((uint32_t)j + 1u < tb ? ld16(P + US * j)
-                                                             : ((uint32_t)j + 1u == tb ? pad_block(P + US * j, rem) : z));
+                                    : ((uint32_t)j + 1u < tb ? ld16(P + USP * j)
+                                                             : ((uint32_t)j + 1u == tb ? pad_block(P + USP * j, rem) : z));
                 }
                 enc_quad<NR, false>(c, x, prev, K.rk, LN, S);
                 const uint32_t nst = q < nq ? 4u : tb;
@@ -486,7 +493,7 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
                         if ((uint32_t)j < nst) st16(C + US * j, c[j]);
                 }
                 prev = c[3];
-                P += 4 * US;
+                P += 4 * USP;
                 C += 4 * US;
                 // the slot is free once the hashing wave has taken every earlier quad
                 if (!RB && count) {

@@ -1015,7 +1015,7 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
             // own, so the 128-B line the two share is read while it is in
             // L2 (one quad apart, an XCD's waves have streamed more than its
             // L2 through and the line is fetched again: 2.7x read traffic)
-            constexpr bool PAIR = RNSTOK_DEC_PAIR && !ILV && !PERKEY;
+            constexpr bool PAIR = RNSTOK_DEC_PAIR && !ILV && !PERKEY && WG <= 768;   // (1024: 11 -> 38 VGPRs spilled)
             u32x4 nx[4];
 #pragma nounroll
             for (uint32_t q = 0; q <= nq; ++q) {

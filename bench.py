@@ -956,6 +956,14 @@ def issue_model(kernel, n, L, keys, n_cu, ms, clock_ghz, pmc=None):
             out["pmc"] = {"issued_slots_per_simd": slots, "slot_cycles": 4 * slots, "kernel_cycles_per_xcd": cyc,
                           "slot_cycles_over_kernel_cycles": 4 * slots / cyc,
                           "dual_issued_frac_of_valu": 2 * pmc["SQ_ACTIVE_INST_VALU2"] / pmc["SQ_INSTS_VALU"]}
+            # two limits (tools/coissue_probe.hip): the SIMDs'
+            # VALU slots, and the CU-wide LDS pipe at 128 B/clk (2 cycles per
+            # wave64 ds_read_b32), which other waves' VALU work can overlap
+            valu_cyc = 4 * (pmc["SQ_INSTS_VALU"] - pmc["SQ_ACTIVE_INST_VALU2"]) / n_simd
+            lds_cyc = 2.0 * pmc["SQ_INSTS_LDS"] / n_cu
+            out["two_limits"] = {"valu_slot_cycles_per_simd": valu_cyc, "lds_pipe_cycles_per_cu": lds_cyc,
+                                 "kernel_cycles": cyc, "valu_share": valu_cyc / cyc, "lds_pipe_share": lds_cyc / cyc,
+                                 "lds_time_hidden_behind_valu": max(0.0, valu_cyc + lds_cyc - cyc) / min(valu_cyc, lds_cyc)}
         except (KeyError, TypeError, ZeroDivisionError):
             pass
     return out

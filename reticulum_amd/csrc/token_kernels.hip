@@ -32,6 +32,9 @@ namespace rnstok {
 #ifndef RNSTOK_SPLIT_TILE            // experiment: packed split encrypt reads 64-packet plaintext tiles
 #define RNSTOK_SPLIT_TILE 0
 #endif
+#ifndef RNSTOK_DEC_TAG_EARLY         // decrypt: tag units loaded before the quad loop
+#define RNSTOK_DEC_TAG_EARLY 1
+#endif
 #ifndef RNSTOK_DEC_PAIR              // decrypt, one key, token quads loaded in pairs: fetch -21 %, time -1.6 %
 #define RNSTOK_DEC_PAIR 1
 #endif
@@ -1007,6 +1010,14 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
             // through one sha256_compress.
             const u32x4 z = {0u, 0u, 0u, 0u};
             u32x4 prev = ld16(Kt);
+            // (RNSTOK_DEC_TAG_EARLY: the tag's two units loaded before the quad
+            // loop, so the compare after it does not wait on them)
+            constexpr bool TAG_EARLY = RNSTOK_DEC_TAG_EARLY && !PERKEY && WG <= 768;
+            u32x4 tag0, tag1;
+            if (TAG_EARLY) {
+                tag0 = ld16(Kt + US * ((T >> 4) - 2u));
+                tag1 = ld16(Kt + US * ((T >> 4) - 1u));
+            }
             const uint8_t *C = Kt + US;
             uint8_t *D = O;
             Sha256 S;
@@ -1055,7 +1066,14 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
             // kept live through the loop), c[0..tb-1] its ciphertext,
             // pp[0..tb-1] its plaintext
             const u32x4 pb = ld16(Kt + 4ull * US * nq);
-            const u32x4 r0 = ld16(Kt + US * ((T >> 4) - 2u)), r1 = ld16(Kt + US * ((T >> 4) - 1u));
+            u32x4 r0, r1;
+            if (TAG_EARLY) {
+                r0 = tag0;
+                r1 = tag1;
+            } else {
+                r0 = ld16(Kt + US * ((T >> 4) - 2u));
+                r1 = ld16(Kt + US * ((T >> 4) - 1u));
+            }
             const u32x4 last = tb == 1u ? pp[0] : (tb == 2u ? pp[1] : (tb == 3u ? pp[2] : pp[3]));
             const bool full = tb >= 3u;
             const uint32_t tu = tb + 1u;

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 4: GPU suite + smoke + default bench line on the paired quad loads,
+# then the headline's kernel trace + PMC passes (rows, default layout).
+set -o pipefail
+O=gpurun_out/r04an
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests -x -v --timeout 120 --timeout-method thread -m gpu > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
+tail -2 $O/gpu_tests.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+cut -c1-300 $O/bench.json
+bash tools/profile.sh r04an > $O/profile.log 2>&1 || { tail -20 $O/profile.log; exit 1; }
+tail -3 $O/profile.log

@@ -389,9 +389,11 @@ void  rt_host_free(void *p);
 int   rt_memcpy_h2d(rt_ctx *ctx, void *dst, const void *src, uint64_t bytes, void *stream);
 int   rt_memcpy_d2h(rt_ctx *ctx, void *dst, const void *src, uint64_t bytes, void *stream);
 /* rt_memcpy_d2h_upto: min(max_bytes, *d_bytes) bytes, the count read on the
- * device at run time (d_bytes: a DEVICE uint64, e.g. frame_off[n] of
- * rt_hdlc_frame, a size the host does not know without a sync), as GPU
- * stores into a pinned `dst` (RT_E_INVAL for any other destination). */
+ * device at run time (d_bytes: a DEVICE 64-bit count on the context's GPU,
+ * e.g. frame_off[n] of rt_hdlc_frame, a size the host does not know without
+ * a sync; read as signed, so zero or negative copies nothing), as GPU stores
+ * into a pinned `dst` (RT_E_INVAL for any other destination); bytes of `dst`
+ * past the count are not written. */
 int   rt_memcpy_d2h_upto(rt_ctx *ctx, void *dst, const void *src, uint64_t max_bytes, const uint64_t *d_bytes,
                          void *stream);
 int   rt_stream_sync(rt_ctx *ctx, void *stream);

@@ -15,8 +15,12 @@ Batch use: ``KeySet.encrypt_batch`` / ``decrypt_batch`` over host buffers,
 device).  Resource hashmaps: ``resource_hashmap`` / ``build_hashmap`` /
 ``get_map_hash`` (Resource.py:426-468, 505-506).  Wire-side neighbours
 (HDLC framing, IFAC masking, packet header unpack/pack): ``reticulum_amd.wire``.
+
+``available()`` tells whether the library and a gfx950 device are usable;
+``reticulum_amd.dropin`` is the import for the reference's one-line swap,
+which raises ImportError when they are not.
 """
-from ._native import NativeError, NativeUnavailable, LIB_PATH  # noqa: F401
+from ._native import NativeError, NativeUnavailable, LIB_PATH, available  # noqa: F401
 from ._native import RT_ST_OK, RT_ST_TOO_SHORT, RT_ST_BAD_HMAC, RT_ST_BAD_CT_LEN, RT_ST_BAD_PAD  # noqa: F401
 from .hkdf import derive_keyset, hkdf, hkdf_batch  # noqa: F401
 from .resource import build_hashmap, get_map_hash, resource_hashmap  # noqa: F401

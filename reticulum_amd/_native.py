@@ -167,3 +167,17 @@ def context(device=None):
                     raise NativeUnavailable(f"rt_create({device}) failed: {last_error()}")
                 _contexts[device] = ctx
     return ctx
+
+
+def available(device=None):
+    """True when librnstok.so loads and a gfx950 device answers rt_create.
+
+    The drop-in import (``reticulum_amd.dropin``) checks this, so a node
+    without the library or the GPU falls back to the reference's Token the
+    way RNS/Cryptography/Provider.py:43-61 always leaves a working backend,
+    instead of every Link.decrypt returning None (RNS/Link.py:1175-1182)."""
+    try:
+        context(device)
+        return True
+    except NativeUnavailable:
+        return False

@@ -22,12 +22,14 @@ typedef unsigned int u32x4c __attribute__((ext_vector_type(4)));
 // dst + head is 16-B aligned; the body is `body` aligned 16-B stores, the
 // head and tail bytes are stored one by one by the first 32 threads.  With
 // `dev_bytes` the byte count is min(bytes, *dev_bytes), read on the device
-// (a size the host does not know, e.g. the end offset of an HDLC stream).
+// (a size the host does not know, e.g. the end offset of an HDLC stream),
+// read as a signed int64 so that a negative count copies nothing.
 __global__ __launch_bounds__(256) void k_store_host(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
                                                     uint64_t bytes, uint32_t head, const uint64_t *dev_bytes) {
     if (dev_bytes) {
-        const uint64_t d = *dev_bytes;
-        bytes = d < bytes ? d : bytes;
+        // a signed count (torch int64): zero or negative copies nothing
+        const int64_t d = (int64_t)*dev_bytes;
+        bytes = d <= 0 ? 0u : ((uint64_t)d < bytes ? (uint64_t)d : bytes);
         head = (uint32_t)(head < bytes ? head : bytes);
     }
     const uint64_t body = (bytes - head) >> 4;

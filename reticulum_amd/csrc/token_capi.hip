@@ -1217,11 +1217,13 @@ int rt_memcpy_d2h_upto(rt_ctx *c, void *dst, const void *src, uint64_t max_bytes
                        void *stream) {
     if (!c || !dst || !src || !d_bytes) return fail(RT_E_INVAL, "rt_memcpy_d2h_upto: null argument");
     RT_HIP(hipSetDevice(c->device), "hipSetDevice");
-    hipPointerAttribute_t ad, as;
+    hipPointerAttribute_t ad, as, an;
     if (!(query(&ad, dst) && ad.type == hipMemoryTypeHost && ad.devicePointer && query(&as, src) &&
           as.type == hipMemoryTypeDevice && as.device == c->device))
         return fail(RT_E_INVAL, "rt_memcpy_d2h_upto: dst must be pinned host memory and src device memory of the "
                                 "context's GPU");
+    if (!(query(&an, d_bytes) && an.type == hipMemoryTypeDevice && an.device == c->device))
+        return fail(RT_E_INVAL, "rt_memcpy_d2h_upto: d_bytes must be device memory of the context's GPU");
     RT_HIP(launch_store_host((uint8_t *)ad.devicePointer, (const uint8_t *)src, max_bytes, pick(c, stream), d_bytes),
            "D2H");
     return RT_OK;

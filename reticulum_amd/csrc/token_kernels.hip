@@ -442,6 +442,7 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
                         while (__hip_atomic_load(consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < count)
                             __builtin_amdgcn_s_sleep(1);
                     ++count;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                     if (lane == 0u) {
                         *chunk_at = 0xFFFFFFFFu;
                         __hip_atomic_store(produced, count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -513,7 +514,9 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
                 }
                 ++count;
                 // lane 0's quad (read back from the token buffer) and the
-                // slot's writes before the count the hashing wave polls
+                // slot's writes before the count the hashing wave polls: every
+                // lane releases its own writes, lane 0 publishes the count
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 if (lane == 0u) {
                     if (GEN && q == 0u) *chunk_at = (uint32_t)base;
                     __hip_atomic_store(produced, count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -569,9 +572,13 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
                     for (int j = 0; j < 4; ++j) c[j] = (act && (uint32_t)j < nst) ? ld16(C + US * j) : z;
                 }
                 ++count;
-                // the slot's reads complete before the AES wave may overwrite it
-                if (!RB && lane == 0u)
-                    __hip_atomic_store(consumed, count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                // the slot's reads (every lane's) complete before the AES wave
+                // may overwrite it
+                if (!RB) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane == 0u)
+                        __hip_atomic_store(consumed, count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
                 C += 4 * US;
                 if (!GEN || q <= nq) {
                     sha_units(w, up, c[0], c[1], c[2]);

@@ -512,14 +512,17 @@ def copy_to_host_upto(dst, src, nbytes_dev, stream=None):
     device tensor ``src`` into the pinned host tensor ``dst``, where
     ``nbytes_dev`` is a one-element int64 DEVICE tensor read at run time (e.g.
     ``frame_off[n]`` from hdlc_frame: the stream's length, which the host
-    does not know without a sync) — GPU stores into the mapped buffer
-    (rt_memcpy_d2h_upto).  Nothing is synchronised."""
+    does not know without a sync; zero or negative copies nothing) — GPU
+    stores into the mapped buffer (rt_memcpy_d2h_upto).  Nothing is
+    synchronised; bytes of ``dst`` past the count are left as they were."""
     if not src.is_cuda or dst.is_cuda or not dst.is_pinned():
         raise ValueError("copy_to_host_upto copies a device tensor into a pinned host tensor")
     if not src.is_contiguous() or not dst.is_contiguous():
         raise ValueError("copy_to_host_upto needs contiguous tensors")
     if nbytes_dev.dtype != torch.int64 or nbytes_dev.numel() != 1 or not nbytes_dev.is_cuda:
         raise TypeError("nbytes_dev: one int64 element on the device")
+    if nbytes_dev.device != src.device:
+        raise ValueError("nbytes_dev must be on src's device")
     nbytes = min(src.numel() * src.element_size(), dst.numel() * dst.element_size())
     if nbytes == 0:
         return

@@ -124,7 +124,13 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
             # (Transport.py:1482-1486); the empty entries past the frames
             # (f_len 0) stay dropped
             un = out
-            flagged = (out[f_off] & 0x80) != 0
+            if out.numel():
+                # flag byte of each frame; entries past the frames (f_len 0)
+                # are never read out of range and never count as flagged
+                first = out[f_off.clamp(0, out.numel() - 1)]
+                flagged = ((first & 0x80) != 0) & (f_len > 0)
+            else:       # an empty read: no frames, nothing to gather
+                flagged = torch.zeros(max_pairs, dtype=torch.bool, device=dev)
             drop = flagged | (f_len <= 2)
             ifac_status = drop.to(torch.int32)
             p_len = torch.where(drop, torch.zeros_like(f_len), f_len)

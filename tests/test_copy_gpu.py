@@ -65,3 +65,40 @@ def test_copy_to_host_ordered_after_kernel_on_stream(dev):
             device.copy_to_host(dst, src, stream=s)
             s.synchronize()
             assert int(dst[0]) == r and int(dst[-1]) == r and bool((dst == r).all())
+
+
+@pytest.mark.parametrize("dst_off", [0, 3, 13])
+def test_copy_to_host_upto_clamps_on_the_device(dev, dst_off):
+    """rt_memcpy_d2h_upto: the count is read on the device and clamped to
+    [0, max]: 0, 1..15 (inside the unaligned head), a middle count, more than
+    the destination holds, and a negative int64 (nothing copied); bytes past
+    the count are untouched."""
+    from reticulum_amd import device
+    size = 4096 + 37
+    g = torch.Generator(device=dev).manual_seed(77 + dst_off)
+    src = torch.randint(0, 256, (size,), dtype=torch.uint8, device=dev, generator=g)
+    ref = src.cpu()
+    for want in [0, 1, 2, 7, 15, 16, 17, 1000, size - 1, size, size + 100, 1 << 40, -1, -4096]:
+        host = torch.full((size + 32,), 0xEE, dtype=torch.uint8).pin_memory()
+        dst = host[dst_off:dst_off + size]
+        nb = torch.tensor([want], dtype=torch.int64, device=dev)
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        device.copy_to_host_upto(dst, src, nb, stream=s)
+        s.synchronize()
+        k = max(0, min(want, size))
+        assert torch.equal(dst[:k], ref[:k]), want
+        assert bool((dst[k:] == 0xEE).all()), want
+        assert bool((host[:dst_off] == 0xEE).all()) and bool((host[dst_off + size:] == 0xEE).all()), want
+
+
+def test_copy_to_host_upto_rejects_bad_counts(dev):
+    from reticulum_amd import device
+    src = torch.zeros(64, dtype=torch.uint8, device=dev)
+    dst = torch.zeros(64, dtype=torch.uint8).pin_memory()
+    with pytest.raises(TypeError):
+        device.copy_to_host_upto(dst, src, torch.tensor([3], dtype=torch.int32, device=dev))
+    with pytest.raises(TypeError):
+        device.copy_to_host_upto(dst, src, torch.tensor([3], dtype=torch.int64))        # on the host
+    with pytest.raises(TypeError):
+        device.copy_to_host_upto(dst, src, torch.tensor([3, 4], dtype=torch.int64, device=dev))

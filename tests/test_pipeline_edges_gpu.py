@@ -218,3 +218,23 @@ def test_inbound_reads_split_across_calls_keep_the_loops_buffer():
         got += [p[o:o + k].tobytes() for o, k in zip(po, pl)]
         carry = data[int(res["counts"][1]):]
     assert got == [pt[i].tobytes() for i in range(n)]
+
+
+@pytest.mark.parametrize("isz", [0, 16])
+def test_inbound_empty_read(isz):
+    """A zero-byte read (the read loop's empty recv) through the whole inbound
+    path: no frames, nothing consumed, every entry empty (the
+    no-IFAC branch gathered each entry's flag byte from an empty buffer)."""
+    import torch
+    import reticulum_amd as rt
+    from reticulum_amd import pipeline
+    dev = torch.device("cuda", 0)
+    ks = rt.KeySet(bytes(range(64)), device=0)
+    ik = torch.arange(64, dtype=torch.uint8, device=dev)
+    res = pipeline.inbound(ks, torch.empty(0, dtype=torch.uint8, device=dev), ik, isz, 4)
+    torch.cuda.synchronize()
+    assert int(res["n_frames"]) == 0
+    assert res["counts"].cpu().tolist() == [0, 0]
+    assert (res["ifac_status"].cpu() == 1).all()
+    assert (res["status"].cpu() == 1).all()
+    assert (res["pt_len"].cpu() == 0).all()

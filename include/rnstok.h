@@ -398,6 +398,21 @@ int   rt_memcpy_d2h_upto(rt_ctx *ctx, void *dst, const void *src, uint64_t max_b
                          void *stream);
 int   rt_stream_sync(rt_ctx *ctx, void *stream);
 
+/* ---- launch clock (measurement; no reference counterpart) ----------------
+ * rt_clock_stamps: from the next launch on, every workgroup of the context's
+ * encrypt and decrypt kernels adds its span to `acc`, a DEVICE buffer of
+ * RT_CLOCK_WORDS uint64 on the context's GPU (null: stop stamping).  Words
+ * [4k .. 4k+3], k = RT_CLOCK_ENCRYPT / RT_CLOCK_DECRYPT: the sum of the
+ * workgroups' spans in shader clock cycles, the same spans in 100 MHz
+ * real-time ticks, the number of workgroups stamped, the number of launches.
+ * The run's sustained shader clock is words[0] / words[1] x 100 MHz and the
+ * cycles per launch words[0] / words[2] (one persistent workgroup per CU).
+ * The caller zeroes `acc` and reads it after the stamped launches complete. */
+#define RT_CLOCK_WORDS 8
+#define RT_CLOCK_ENCRYPT 0
+#define RT_CLOCK_DECRYPT 1
+int   rt_clock_stamps(rt_ctx *ctx, uint64_t *acc);
+
 #ifdef __cplusplus
 }
 #endif

@@ -72,6 +72,7 @@ SIGNATURES = [
     ("rt_memcpy_d2h", _int, [_vp, _vp, _vp, _u64, _vp]),
     ("rt_memcpy_d2h_upto", _int, [_vp, _vp, _vp, _u64, _vp, _vp]),
     ("rt_stream_sync", _int, [_vp, _vp]),
+    ("rt_clock_stamps", _int, [_vp, _vp]),
 ]
 
 

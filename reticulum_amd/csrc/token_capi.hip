@@ -91,6 +91,8 @@ struct rt_ctx {
     Stager stagers[N_STAGERS];
     std::atomic<uint32_t> stager_rr{0};
     QueueRing queues;
+    // rt_clock_stamps: the launch-clock words the token kernels add to, or null
+    std::atomic<unsigned long long *> clk{nullptr};
 };
 
 // Takes a free staging lane (or waits for the caller's round-robin one).
@@ -447,6 +449,7 @@ static int enc_common(const rt_keyset *k, EncArgs &a, void *stream) {
     if ((!a.pt && (a.pt_len || a.uni_len)) || !a.iv || !a.tok) return fail(RT_E_INVAL, "rt_encrypt: null buffer");
     a.rec = k->d_rec;
     a.sbox = k->ctx->d_sbox;
+    if (unsigned long long *w = k->ctx->clk.load(std::memory_order_acquire)) a.clk = w + 4 * RT_CLOCK_ENCRYPT;
     hipStream_t s = pick(k->ctx, stream);
     RT_HIP(hipSetDevice(k->ctx->device), "hipSetDevice");
     RT_HIP(after_setup(k, s), "wait for key setup");
@@ -462,6 +465,7 @@ static int dec_common(const rt_keyset *k, DecArgs &a, void *stream) {
     if (!a.tok || !a.pt || !a.out_len || !a.status) return fail(RT_E_INVAL, "rt_decrypt: null buffer");
     a.rec = k->d_rec;
     a.sbox = k->ctx->d_sbox;
+    if (unsigned long long *w = k->ctx->clk.load(std::memory_order_acquire)) a.clk = w + 4 * RT_CLOCK_DECRYPT;
     hipStream_t s = pick(k->ctx, stream);
     RT_HIP(hipSetDevice(k->ctx->device), "hipSetDevice");
     RT_HIP(after_setup(k, s), "wait for key setup");
@@ -1226,6 +1230,17 @@ int rt_memcpy_d2h_upto(rt_ctx *c, void *dst, const void *src, uint64_t max_bytes
         return fail(RT_E_INVAL, "rt_memcpy_d2h_upto: d_bytes must be device memory of the context's GPU");
     RT_HIP(launch_store_host((uint8_t *)ad.devicePointer, (const uint8_t *)src, max_bytes, pick(c, stream), d_bytes),
            "D2H");
+    return RT_OK;
+}
+int rt_clock_stamps(rt_ctx *c, uint64_t *acc) {
+    if (!c) return fail(RT_E_INVAL, "null context");
+    if (acc) {
+        RT_HIP(hipSetDevice(c->device), "hipSetDevice");
+        hipPointerAttribute_t at;
+        if (((uintptr_t)acc & 7u) || !(query(&at, acc) && at.type == hipMemoryTypeDevice && at.device == c->device))
+            return fail(RT_E_INVAL, "rt_clock_stamps: acc must be 8-byte aligned device memory of the context's GPU");
+    }
+    c->clk.store((unsigned long long *)acc, std::memory_order_release);
     return RT_OK;
 }
 int rt_stream_sync(rt_ctx *c, void *stream) {

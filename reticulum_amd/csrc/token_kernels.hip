@@ -192,6 +192,38 @@ __device__ __forceinline__ uint32_t take_chunk(uint32_t *q) {
                   rt_i_ = rt_base_ + (threadIdx.x & 63u))                                                     \
         if (const uint32_t I = (uint32_t)rt_i_; true)
 
+// ------------------------------------------------------------ launch clock --
+//
+// rt_clock_stamps: each workgroup of a stamped launch adds its span in shader
+// clock cycles (s_memtime) and in 100 MHz real-time ticks (s_memrealtime) to
+// its kernel class's words: {sum of cycles, sum of ticks, workgroups, launches}.
+// The sustained clock of the run is cycles / ticks x 100 MHz and the cycles per
+// launch the mean workgroup span (one persistent workgroup per CU), measured
+// in the run itself instead of read from a profile of another box.  The end
+// stamp follows a workgroup barrier, so the span covers every wave; the
+// uniform pointer keeps the branch (and the barrier) wave- and
+// workgroup-uniform.  Off (null), it costs one scalar compare per launch.
+struct LaunchClock {
+    uint64_t c0 = 0, r0 = 0;
+    __device__ __forceinline__ void start(const unsigned long long *acc) {
+        if (acc) {
+            c0 = __builtin_amdgcn_s_memtime();
+            r0 = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+    __device__ __forceinline__ void finish(unsigned long long *acc) const {
+        if (!acc) return;
+        __syncthreads();
+        if (threadIdx.x == 0u) {
+            const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+            __hip_atomic_fetch_add(acc + 0, (unsigned long long)(c1 - c0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(acc + 1, (unsigned long long)(r1 - r0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(acc + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (blockIdx.x == 0u) __hip_atomic_fetch_add(acc + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+};
+
 // PKCS7 pad block (PKCS7.py:35-39): r (< 16) payload bytes at p, then 16-r copies of 16-r.
 __device__ __forceinline__ u32x4 pad_block(const uint8_t *p, uint32_t r) {
     uint32_t n = 16u - r, w[4] = {0, 0, 0, 0};
@@ -214,6 +246,8 @@ __device__ __forceinline__ u32x4 pad_block(const uint8_t *p, uint32_t r) {
 template <int NR, bool PERKEY, bool ILV = false>
 __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encrypt(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
+    LaunchClock clk;
+    clk.start(a.clk);
     fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);
     const Lanes LN(threadIdx.x & 31u);
 
@@ -323,6 +357,7 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
             st16(T + US, u32x4{bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7])});
         }
     }
+    clk.finish(a.clk);
 }
 
 // ----------------------------------------------------- encrypt, split roles --
@@ -405,6 +440,8 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
     const uint32_t slot = SPLIT_RING + 4096u * pair;
     lds_u32 *produced = (lds_u32 *)(uintptr_t)slot, *consumed = (lds_u32 *)(uintptr_t)(slot + 4u);
     lds_u32 *chunk_at = (lds_u32 *)(uintptr_t)(slot + 8u);
+    LaunchClock clk;
+    clk.start(a.clk);
     if (aes && lane < 3u) ((lds_u32 *)(uintptr_t)slot)[lane] = 0u;   // before the barrier
     fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);     // ends with the workgroup barrier
     SPLIT_PROBE(uint64_t pr_wait = 0; uint64_t pr_n = 0; const uint64_t pr_t0 = clock64();)
@@ -616,6 +653,7 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
         atomicAdd(&g_split_probe[6 + r], 1ull);
     }
 #endif
+    clk.finish(a.clk);
 }
 
 // ---------------------------------------------------- encrypt, long tokens --
@@ -959,6 +997,8 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
 template <int NR, bool PERKEY, int WG = PERKEY ? WG_PERKEY_DEC : WG_DEC, bool ILV = false>
 __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
+    LaunchClock clk;
+    clk.start(a.clk);
     fill_tables<true>(tab_u32, a.sbox, a.sbox + 256);
     const Lanes LN(threadIdx.x & 31u);
 
@@ -1107,6 +1147,7 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
         a.status[p] = st;
         a.out_len[p] = outlen;
     }
+    clk.finish(a.clk);
 }
 
 // ---------------------------------------------------- decrypt, long tokens --

@@ -22,6 +22,7 @@ struct EncArgs {
     uint32_t *queue;            // null -> static grid stride; else a zeroed chunk counter (sorted batches)
     uint32_t n;
     uint32_t ilv;               // 1: unit-interleaved layout (16-B unit u of packet p at 16*(u*n + p)), uniform
+    unsigned long long *clk;    // null, or this kernel class's 4 launch-clock words (rt_clock_stamps)
 };
 
 struct DecArgs {
@@ -42,6 +43,7 @@ struct DecArgs {
     uint32_t *queue;            // as EncArgs::queue
     uint32_t n;
     uint32_t ilv;               // as EncArgs::ilv (tokens and plaintexts), well-formed uniform tokens only
+    unsigned long long *clk;    // as EncArgs::clk
 };
 
 // Ratchet trials (Identity.py:865-878): pairs j in [pair_off[t],

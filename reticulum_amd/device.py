@@ -529,3 +529,59 @@ def copy_to_host_upto(dst, src, nbytes_dev, stream=None):
     lib = _native.load()
     _native.check(lib.rt_memcpy_d2h_upto(_ctx_of(src), dst.data_ptr(), src.data_ptr(), nbytes, _p(nbytes_dev),
                                          _stream(stream, src.device)))
+
+
+# ------------------------------------------------------------ launch clock --
+
+CLOCK_KERNELS = ("encrypt", "decrypt")      # RT_CLOCK_ENCRYPT, RT_CLOCK_DECRYPT
+REALTIME_HZ = 100e6                         # s_memrealtime ticks per second
+
+
+def clock_summary(words):
+    """The rt_clock_stamps words (8 ints) as per-kernel figures: the run's
+    sustained shader clock (cycles / real-time ticks x 100 MHz), the cycles
+    per launch (the mean workgroup span: one persistent workgroup per CU)
+    and the mean workgroup span in ms.  Kernels with no stamped launch are
+    left out."""
+    out = {}
+    for k, name in enumerate(CLOCK_KERNELS):
+        cyc, ticks, wgs, launches = (int(x) for x in words[4 * k:4 * k + 4])
+        if wgs == 0 or ticks == 0:
+            continue
+        out[name] = {"clock_ghz": cyc / ticks * REALTIME_HZ / 1e9, "cycles_per_launch": cyc / wgs,
+                     "wg_span_ms": ticks / wgs / REALTIME_HZ * 1e3, "launches": launches,
+                     "workgroups_per_launch": wgs / launches if launches else None}
+    return out
+
+
+class LaunchClock:
+    """Stamp every encrypt/decrypt launch of a block on ``device``'s context
+    (rt_clock_stamps) and read the run's clock afterwards::
+
+        with device.LaunchClock(dev) as lc:
+            ...launches...
+        lc.summary()      # syncs the device, then clock_summary(words)
+    """
+
+    def __init__(self, dev=None):
+        dev = torch.device("cuda", torch.cuda.current_device()) if dev is None else torch.device(dev)
+        self.dev = dev
+        self.acc = torch.zeros(8, dtype=torch.int64, device=dev)
+        self._ctx = _native.context(dev.index if dev.index is not None else torch.cuda.current_device())
+
+    def __enter__(self):
+        # the zeroed words are ordered before any launch the block enqueues
+        torch.cuda.synchronize(self.dev)
+        _native.check(_native.load().rt_clock_stamps(self._ctx, self.acc.data_ptr()))
+        return self
+
+    def __exit__(self, *exc):
+        _native.check(_native.load().rt_clock_stamps(self._ctx, None))
+        return False
+
+    def words(self):
+        torch.cuda.synchronize(self.dev)
+        return [int(x) for x in self.acc.cpu()]
+
+    def summary(self):
+        return clock_summary(self.words())

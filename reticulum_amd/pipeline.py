@@ -99,7 +99,9 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
     between frames would otherwise be half of every wave)."""
     with _on(stream):      # temporaries allocated on the stream that uses them
         dev = buf.device
-        out = torch.empty(buf.numel(), dtype=torch.uint8, device=dev)
+        # (at least one byte: an empty read still gives every later stage a
+        # buffer to point at; no frame ever reaches into it)
+        out = torch.empty(max(buf.numel(), 1), dtype=torch.uint8, device=dev)
         d_off = torch.empty(max_pairs, dtype=torch.int64, device=dev)
         d_len = torch.empty(max_pairs, dtype=torch.int32, device=dev)
         d_st = torch.full((max_pairs,), -1, dtype=torch.int32, device=dev)
@@ -124,13 +126,10 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
             # (Transport.py:1482-1486); the empty entries past the frames
             # (f_len 0) stay dropped
             un = out
-            if out.numel():
-                # flag byte of each frame; entries past the frames (f_len 0)
-                # are never read out of range and never count as flagged
-                first = out[f_off.clamp(0, out.numel() - 1)]
-                flagged = ((first & 0x80) != 0) & (f_len > 0)
-            else:       # an empty read: no frames, nothing to gather
-                flagged = torch.zeros(max_pairs, dtype=torch.bool, device=dev)
+            # flag byte of each frame; entries past the frames (f_len 0, f_off
+            # unspecified) are never read out of range and never count as flagged
+            first = out[f_off.clamp(0, out.numel() - 1)]
+            flagged = ((first & 0x80) != 0) & (f_len > 0)
             drop = flagged | (f_len <= 2)
             ifac_status = drop.to(torch.int32)
             p_len = torch.where(drop, torch.zeros_like(f_len), f_len)

@@ -1258,16 +1258,20 @@ def shard_rate(dev, n_cu, steps=10, L=16384, per_cu=128):
     for name, f, ops in (("encrypt", enc, ops_enc(L)), ("decrypt", dec, ops_dec(L))):
         warmup(f, stream, 2, 0.3)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-        for a, b in ev:
-            a.record(stream)
-            f()
-            b.record(stream)
-        torch.cuda.synchronize()
+        with device.LaunchClock(dev) as lc:
+            for a, b in ev:
+                a.record(stream)
+                f()
+                b.record(stream)
+            torch.cuda.synchronize()
         ms = sorted(a.elapsed_time(b) for a, b in ev)[steps // 2]
-        res[name] = {"ms": ms, "tokens_s": n / (ms * 1e-3), "frac_of_valu_peak": ops * n / (ms * 1e-3) / peak}
+        clk = lc.summary().get(name, {})
+        res[name] = {"ms": ms, "tokens_s": n / (ms * 1e-3), "frac_of_valu_peak": ops * n / (ms * 1e-3) / peak,
+                     "clock_ghz": clk.get("clock_ghz"), "cycles_per_launch": clk.get("cycles_per_launch")}
     res["note"] = ("one rank's share of c4 at 8 GPUs; CBC encryption is a serial chain per token, so this shape "
                    "is bound by the chain's round latency, not by issue (DESIGN.md \u00a74.2); kernels = "
-                   "RT_KERNEL_* from rt_plan_uniform")
+                   "RT_KERNEL_* from rt_plan_uniform; clock_ghz / cycles_per_launch stamped by the kernels in "
+                   "this run (rt_clock_stamps)")
     return res
 
 

@@ -400,7 +400,8 @@ int   rt_stream_sync(rt_ctx *ctx, void *stream);
 
 /* ---- launch clock (measurement; no reference counterpart) ----------------
  * rt_clock_stamps: from the next launch on, every workgroup of the context's
- * encrypt and decrypt kernels adds its span to `acc`, a DEVICE buffer of
+ * encrypt and decrypt kernels (the one-packet-per-lane, split and long-token
+ * kernels of rt_encrypt* / rt_decrypt*) adds its span to `acc`, a DEVICE buffer of
  * RT_CLOCK_WORDS uint64 on the context's GPU (null: stop stamping).  Words
  * [4k .. 4k+3], k = RT_CLOCK_ENCRYPT / RT_CLOCK_DECRYPT: the sum of the
  * workgroups' spans in shader clock cycles, the same spans in 100 MHz

@@ -689,6 +689,8 @@ __global__ __launch_bounds__(256) void k_encrypt_long(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
     typedef __attribute__((address_space(3))) uint32_t lds_word;
     lds_word *max_steps = (lds_word *)(uintptr_t)STEP_WORD;
+    LaunchClock clk;
+    clk.start(a.clk);
     fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);
     const Lanes LN(threadIdx.x & 31u);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
@@ -793,6 +795,7 @@ __global__ __launch_bounds__(256) void k_encrypt_long(EncArgs a) {
             }
         }
     }
+    clk.finish(a.clk);
 }
 
 // ------------------------------------ encrypt, long tokens, 4 lanes/token --
@@ -889,6 +892,8 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
     typedef __attribute__((address_space(3))) uint32_t lds_w;
     typedef __attribute__((address_space(3))) const u32x4 lds_q;
+    LaunchClock clk;
+    clk.start(a.clk);
     fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);
     const Lanes LN(threadIdx.x & 31u);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
@@ -985,6 +990,7 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
             }
         }
     }
+    clk.finish(a.clk);
 }
 
 // --------------------------------------------------------------- decrypt --
@@ -1270,6 +1276,8 @@ __device__ __forceinline__ void dl2_signal(uint32_t flag_addr, uint32_t v) {
 template <int NR>
 __global__ __launch_bounds__(DL2_THREADS) void k_decrypt_long2(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab_u32[];
+    LaunchClock clk;
+    clk.start(a.clk);
     fill_tables_dl2(tab_u32, a.sbox + 256);
     const Lanes LN(threadIdx.x & 31u);
     const uint32_t inv_off = DL2_INVS | (4u * (threadIdx.x & 15u));
@@ -1448,6 +1456,9 @@ __global__ __launch_bounds__(DL2_THREADS) void k_decrypt_long2(DecArgs a) {
         if (threadIdx.x < 16u) tab_u32[(DL2_FLAGS >> 2) + threadIdx.x] = 0u;     // counters restart per batch
         __syncthreads();
     }
+#ifndef RNSTOK_DL2_PROBE_AES_ONLY
+    clk.finish(a.clk);
+#endif
 }
 
 // --------------------------------------------------------- ratchet trials --

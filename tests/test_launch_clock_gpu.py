@@ -77,3 +77,25 @@ def test_clock_stamps_rejects_host_memory():
     buf = (ctypes.c_uint64 * 8)()
     assert lib.rt_clock_stamps(_native.context(0), ctypes.addressof(buf)) < 0
     assert lib.rt_clock_stamps(_native.context(0), None) == 0
+
+
+def test_launch_clock_stamps_long_token_kernels():
+    """Batches of few packets per CU route to the long-token kernels
+    (k_encrypt_long4 / k_decrypt_long2 for one key, k_encrypt_long per key):
+    they stamp their launches too."""
+    import reticulum_amd as rt
+    from reticulum_amd import device, _native
+    dev, ks, pt, iv, tok, back, ol, st, L, tl = _batch(1024, 500)
+    lib, ctx = _native.load(), _native.context(0)
+    assert lib.rt_plan_uniform(ctx, 1024, L, 0, 0) == _native.RT_KERNEL_ENC_LONG4
+    assert lib.rt_plan_uniform(ctx, 1024, tl, 0, 1) == _native.RT_KERNEL_DEC_LONG2
+    with device.LaunchClock(dev) as lc:
+        device.encrypt_uniform(ks, pt, L, iv, tok)
+        device.decrypt_uniform(ks, tok, tl, back, ol, st)
+        kk = rt.KeySet([bytes(range(64)), bytes(range(64, 128))], device=0)     # two keys: the per-key long kernel
+        kidx = (torch.arange(1024, device=dev, dtype=torch.int32) & 1).contiguous()
+        device.encrypt_uniform(kk, pt, L, iv, tok, key_idx=kidx)
+    s = lc.summary()
+    assert bool((st == 0).all()) and torch.equal(back[:, :L], pt)
+    assert s["encrypt"]["launches"] == 2 and s["decrypt"]["launches"] == 1, s
+    assert 0.5 < s["encrypt"]["clock_ghz"] < 2.6 and 0.5 < s["decrypt"]["clock_ghz"] < 2.6, s

@@ -38,6 +38,12 @@ namespace rnstok {
 #ifndef RNSTOK_DEC_PAIR              // decrypt, one key, token quads loaded in pairs: fetch -21 %, time -1.6 %
 #define RNSTOK_DEC_PAIR 1
 #endif
+#ifndef RNSTOK_SPLIT_DYN              // split encrypt: unevenly divided uniform batches from a counter
+#define RNSTOK_SPLIT_DYN 1
+#endif
+#ifndef RNSTOK_SPLIT_DYN_MIN_LEN
+#define RNSTOK_SPLIT_DYN_MIN_LEN 256u
+#endif
 #ifndef RNSTOK_WG_ENC
 #define RNSTOK_WG_ENC 1024      // single key: 4 waves/SIMD, 128 VGPRs
 #endif
@@ -1876,6 +1882,8 @@ template <class Args>
 static hipError_t balance(Args &a, Shape sh, SpareQueue *spare, hipStream_t s, bool *took, uint32_t *slot) {
     const uint64_t lanes = (uint64_t)sh.grid * (uint64_t)sh.threads;
     *took = false;
+    // (whole passes keep the static stride: the counter measured -4..-7 % at
+    // 5 and 6 passes but +2.3 % at 4 on two boxes, profiles/r05h_dyn/)
     if (a.queue || !spare || a.n <= lanes || a.n % lanes == 0 || a.n > QUEUE_MAX_N) return hipSuccess;
     a.queue = spare->acquire(s, slot);
     if (!a.queue) return hipSuccess;     // no slot: the static stride (correct, less balanced)
@@ -1903,8 +1911,34 @@ hipError_t launch_encrypt(const EncArgs &args, int nr, int n_cu, SpareQueue *spa
     if (plan == RT_KERNEL_ENC_LONG)
         return nr == 14 ? launch_enc_long_nr<14>(a, n_cu, s) : launch_enc_long_nr<10>(a, n_cu, s);
 
-    if (use_split_enc(a, n_cu))
-        return nr == 14 ? launch_enc_split_nr<14>(a, n_cu, s) : launch_enc_split_nr<10>(a, n_cu, s);
+    if (use_split_enc(a, n_cu)) {
+        // Uniform row batches that do not give every AES wave the same number
+        // of 64-packet batches take them from a chunk counter instead of the
+        // static stride, as k_decrypt's ragged batches do (balance): 2^20 x
+        // 500 B (8 per AES wave) keeps the stride; 983 040 x 500 B (7.5 per
+        // wave) -4.8..-5.8 %, 1.5 M x 500 B -4.6..-10 % on three boxes
+        // (profiles/r05h_dyn/).  Short packets keep the stride: a counter
+        // fetch is an L2 round trip per batch, +18 % at 100 B.
+        const bool gen = a.pt_len || a.order || a.queue || a.pt_off;
+        const uint64_t waves = split_grid(a.n, n_cu) * SPLIT_AES_WAVES, batches = (a.n + 63ull) / 64ull;
+        bool took = false;
+        uint32_t slot = 0;
+        if (RNSTOK_SPLIT_DYN && !gen && !a.ilv && spare && a.n <= QUEUE_MAX_N && batches % waves != 0 &&
+            a.uni_len >= RNSTOK_SPLIT_DYN_MIN_LEN) {
+            a.queue = spare->acquire(s, &slot);
+            took = a.queue != nullptr;
+            if (took) {
+                hipError_t e = hipMemsetAsync(a.queue, 0, 4, s);
+                if (e != hipSuccess) {
+                    spare->release(s, slot);
+                    return e;
+                }
+            }
+        }
+        hipError_t e = nr == 14 ? launch_enc_split_nr<14>(a, n_cu, s) : launch_enc_split_nr<10>(a, n_cu, s);
+        if (took) spare->release(s, slot);
+        return e;
+    }
     const Shape sh = shape_for(a.n, a.key_idx ? WG_PERKEY_ENC : WG_ENC, n_cu);
     bool took = false;
     uint32_t slot = 0;

@@ -37,7 +37,11 @@ def _split_n(extra):
 @pytest.mark.parametrize("L,klen,extra,n_keys", [(500, 64, 0, 1), (500, 64, 37, 1), (0, 64, 5, 1), (15, 64, 63, 1),
                                                  (16, 32, 64, 1), (17, 64, 1, 1), (100, 32, 0, 1), (1500, 64, 129, 1),
                                                  (63, 64, 3, 1), (500, 64, 11, 97), (100, 32, 64, 5), (1, 64, 0, 65536),
-                                                 (128, 64, 9, 1), (143, 64, 0, 1), (191, 32, 2, 1)])
+                                                 (128, 64, 9, 1), (143, 64, 0, 1), (191, 32, 2, 1),
+                                                 # AES waves unevenly loaded (1.5 / 1.53 batches per wave): the
+                                                 # row layout takes its batches from a chunk counter, the
+                                                 # interleaved one keeps the static stride
+                                                 (500, 64, 65541, 1), (1000, 32, 70000, 1), (256, 64, 65600, 3)])
 def test_split_kernels_tokens_and_round_trip(rt, L, klen, extra, n_keys):
     import torch
     from reticulum_amd import _native, device

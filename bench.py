@@ -364,7 +364,7 @@ def main():
     # once on its own shard, over its own PCIe link (the node's host-origin rate)
     # (N > 1: below, after the headline line exists, under a deadline)
     e2e = e2e_rate(ks, pt, iv, L, tl, n, stream) if args.e2e and world == 1 else None
-    node = shard8 = c5share = c3leg = None
+    node = shard8 = c5share = c3leg = percall = None
     if args.node and world == 1 and args.config == "c2":
         try:
             node = node_rate(dev)
@@ -386,6 +386,10 @@ def main():
             c3leg = c3_rate(dev, _native.load().rt_num_cus(_native.context(local)))
         except Exception as exc:
             c3leg = {"error": f"{type(exc).__name__}: {exc}"}
+        try:
+            percall = per_call_rate()
+        except Exception as exc:
+            percall = {"error": f"{type(exc).__name__}: {exc}"}
 
     lib = _native.load()
     n_cu = lib.rt_num_cus(_native.context(local))
@@ -494,6 +498,7 @@ def main():
         "c4_rank_share_8gpu": shard8,
         "c5_rank_share_8gpu": c5share,
         "c3_per_key": c3leg,
+        "per_call_threads": percall,
         "sharded_c4": None,
     }
 
@@ -1272,6 +1277,53 @@ def shard_rate(dev, n_cu, steps=10, L=16384, per_cu=128):
                    "is bound by the chain's round latency, not by issue (DESIGN.md \u00a74.2); kernels = "
                    "RT_KERNEL_* from rt_plan_uniform; clock_ghz / cycles_per_launch stamped by the kernels in "
                    "this run (rt_clock_stamps)")
+    return res
+
+
+def per_call_rate(threads=16, calls=200, L=383, seconds_cap=20.0):
+    """The reference's call pattern (RNS/Link.py:1161-1182: one synchronous
+    Token call per packet, from many interface and application threads):
+    ``threads`` threads, each with its own link key, alternately encrypting a
+    ``L``-byte packet and decrypting the token, through ``Token`` (one GPU
+    round trip per call; the host entry points' four staging lanes let four
+    run at once) and through ``coalesce.CoalescingToken`` (group commit: the
+    calls waiting at a moment share one launch).  Calls/s over all threads,
+    and the coalescer's mean batch."""
+    import threading
+    import reticulum_amd as rt
+    from reticulum_amd import coalesce
+    res = {"threads": threads, "calls_per_thread": calls, "plaintext_bytes": L}
+    for name, cls in (("token", rt.Token), ("coalescing_token", coalesce.CoalescingToken)):
+        coalesce._coalescers.clear()
+        toks = [cls(os.urandom(64)) for _ in range(threads)]
+        pts = [os.urandom(L) for _ in range(threads)]
+        for t, p in zip(toks, pts):                      # key sets built, kernels warm
+            assert t.decrypt(t.encrypt(p)) == p
+        bad = []
+        barrier = threading.Barrier(threads + 1)
+        deadline = time.perf_counter() + seconds_cap
+
+        def work(i):
+            t, p = toks[i], pts[i]
+            barrier.wait()
+            for _ in range(calls // 2):
+                if t.decrypt(t.encrypt(p)) != p:
+                    bad.append(i)
+                if time.perf_counter() > deadline:
+                    break
+        th = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+        for x in th:
+            x.start()
+        barrier.wait()
+        t0 = time.perf_counter()
+        for x in th:
+            x.join()
+        el = time.perf_counter() - t0
+        st = coalesce.coalescer().stats if cls is coalesce.CoalescingToken else None
+        res[name] = {"calls_s": threads * (calls // 2) * 2 / el, "seconds": el, "ok": not bad,
+                     "mean_batch": (st["calls"] / st["batches"]) if st and st["batches"] else None}
+    res["note"] = ("one synchronous Token call per packet, as Link.encrypt/decrypt make them, from many threads; "
+                   "host buffers, copies included; calls_s counts encrypts and decrypts")
     return res
 
 

@@ -1284,23 +1284,19 @@ def per_call_rate(threads=16, calls=200, L=383, seconds_cap=20.0):
     """The reference's call pattern (RNS/Link.py:1161-1182: one synchronous
     Token call per packet, from many interface and application threads):
     ``threads`` threads, each with its own link key, alternately encrypting a
-    ``L``-byte packet and decrypting the token, through ``Token`` (one GPU
+    ``L``-byte packet and decrypting the token through ``Token`` (one GPU
     round trip per call; the host entry points' four staging lanes let four
-    run at once) and through ``coalesce.CoalescingToken`` (group commit: the
-    calls waiting at a moment share one launch).  Calls/s over all threads,
-    and the coalescer's mean batch."""
+    run at once), and the same from one thread.  Calls/s over all threads."""
     import threading
     import reticulum_amd as rt
-    from reticulum_amd import coalesce
-    res = {"threads": threads, "calls_per_thread": calls, "plaintext_bytes": L}
-    for name, cls in (("token", rt.Token), ("coalescing_token", coalesce.CoalescingToken)):
-        coalesce._coalescers.clear()
-        toks = [cls(os.urandom(64)) for _ in range(threads)]
-        pts = [os.urandom(L) for _ in range(threads)]
+    res = {"plaintext_bytes": L}
+    for name, n_th in (("threads", threads), ("one_thread", 1)):
+        toks = [rt.Token(os.urandom(64)) for _ in range(n_th)]
+        pts = [os.urandom(L) for _ in range(n_th)]
         for t, p in zip(toks, pts):                      # key sets built, kernels warm
             assert t.decrypt(t.encrypt(p)) == p
-        bad = []
-        barrier = threading.Barrier(threads + 1)
+        bad, done = [], [0] * n_th
+        barrier = threading.Barrier(n_th + 1)
         deadline = time.perf_counter() + seconds_cap
 
         def work(i):
@@ -1309,9 +1305,10 @@ def per_call_rate(threads=16, calls=200, L=383, seconds_cap=20.0):
             for _ in range(calls // 2):
                 if t.decrypt(t.encrypt(p)) != p:
                     bad.append(i)
+                done[i] += 2
                 if time.perf_counter() > deadline:
                     break
-        th = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+        th = [threading.Thread(target=work, args=(i,)) for i in range(n_th)]
         for x in th:
             x.start()
         barrier.wait()
@@ -1319,11 +1316,9 @@ def per_call_rate(threads=16, calls=200, L=383, seconds_cap=20.0):
         for x in th:
             x.join()
         el = time.perf_counter() - t0
-        st = coalesce.coalescer().stats if cls is coalesce.CoalescingToken else None
-        res[name] = {"calls_s": threads * (calls // 2) * 2 / el, "seconds": el, "ok": not bad,
-                     "mean_batch": (st["calls"] / st["batches"]) if st and st["batches"] else None}
-    res["note"] = ("one synchronous Token call per packet, as Link.encrypt/decrypt make them, from many threads; "
-                   "host buffers, copies included; calls_s counts encrypts and decrypts")
+        res[name] = {"threads": n_th, "calls_s": sum(done) / el, "seconds": el, "ok": not bad}
+    res["note"] = ("one synchronous Token call per packet, as Link.encrypt/decrypt make them; host buffers, copies "
+                   "included; calls_s counts encrypts and decrypts (DESIGN.md \u00a74.2, INTEGRATION.md \u00a71)")
     return res
 
 

@@ -77,7 +77,8 @@ def test_uncontended_call_is_a_batch_of_one(monkeypatch):
     t = coalesce.CoalescingToken(key)
     tok = t.encrypt(b"hello")
     assert t.decrypt(tok) == b"hello"
-    assert coalesce.coalescer().stats == {"calls": 2, "batches": 2}
+    st = coalesce.coalescer().stats
+    assert (st["calls"], st["batches"], st["key_tables"]) == (2, 2, 0)      # the plain Token calls
     assert [c for c in fake.calls if c[0] in ("encrypt", "decrypt")] == [("encrypt", 1), ("decrypt", 1)]
 
 
@@ -86,7 +87,7 @@ def test_queued_calls_share_one_batch(monkeypatch):
     batch together (group commit)."""
     fake = fake_native.install(monkeypatch)
     from reticulum_amd import coalesce
-    c = coalesce.Coalescer()
+    c = coalesce.Coalescer(leaders=1)
     gate, entered = threading.Event(), threading.Event()
     orig = fake.rt_encrypt_host
 
@@ -96,11 +97,12 @@ def test_queued_calls_share_one_batch(monkeypatch):
         return orig(*a)
     monkeypatch.setattr(fake, "rt_encrypt_host", slow)
     key = os.urandom(64)
+    tok = coalesce.CoalescingToken(key)
     out = {}
-    first = threading.Thread(target=lambda: out.setdefault("first", c.run(coalesce._ENC, key, b"a")))
+    first = threading.Thread(target=lambda: out.setdefault("first", c.run(coalesce._ENC, coalesce.CoalescingToken(key), b"a")))
     first.start()
     assert entered.wait(10)
-    rest = [threading.Thread(target=lambda i=i: out.setdefault(i, c.run(coalesce._ENC, key, bytes([i]) * i)))
+    rest = [threading.Thread(target=lambda i=i: out.setdefault(i, c.run(coalesce._ENC, tok, bytes([i]) * i)))
             for i in range(1, 9)]
     for x in rest:
         x.start()
@@ -110,11 +112,29 @@ def test_queued_calls_share_one_batch(monkeypatch):
     first.join()
     for x in rest:
         x.join()
-    assert c.stats == {"calls": 9, "batches": 2}
+    assert (c.stats["calls"], c.stats["batches"]) == (9, 2)
     assert [n for op, n in fake.calls if op == "encrypt"] == [1, 8]
     for i in range(1, 9):
         s, p = ctoken.decrypt(key, out[i])
         assert s == 0 and p == bytes([i]) * i
+
+
+def test_key_table_is_rebuilt_only_for_new_keys(monkeypatch):
+    fake_native.install(monkeypatch)
+    from reticulum_amd import coalesce
+    c = coalesce.Coalescer(max_keys=3)
+    keys = [os.urandom(64) for _ in range(5)]
+    toks = [coalesce.CoalescingToken(k) for k in keys]
+    for a, b in ((0, 1), (1, 2), (2, 0)):                        # batches of two (a batch of one is the plain call)
+        c._execute([coalesce._Call(coalesce._ENC, toks[a], b"x"), coalesce._Call(coalesce._ENC, toks[b], b"x")])
+    assert c.stats["key_tables"] == 2                            # built for keys 0, 1; rebuilt for key 2
+    calls = [coalesce._Call(coalesce._ENC, toks[i % 3], b"y") for i in range(6)]
+    c._execute(calls)
+    for i, cl in enumerate(calls):
+        assert ctoken.decrypt(keys[i % 3], cl.result) == (0, b"y")
+    assert c.stats["key_tables"] == 2                            # known keys: no rebuild
+    c._execute([coalesce._Call(coalesce._ENC, toks[3], b"z"), coalesce._Call(coalesce._ENC, toks[4], b"z")])
+    assert c.stats["key_tables"] == 3 and list(c._tables[64][1]) == [keys[3], keys[4]]   # past max_keys: restart
 
 
 def test_type_and_key_errors_as_token():

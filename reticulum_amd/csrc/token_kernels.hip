@@ -44,6 +44,9 @@ namespace rnstok {
 #ifndef RNSTOK_SPLIT_DYN_MIN_LEN
 #define RNSTOK_SPLIT_DYN_MIN_LEN 256u
 #endif
+#ifndef RNSTOK_DEC1024_MAX_TOKEN     // uniform tokens up to this length: the 1024-thread decrypt
+#define RNSTOK_DEC1024_MAX_TOKEN 320u  // (plaintexts up to 271 B)
+#endif
 #ifndef RNSTOK_WG_ENC
 #define RNSTOK_WG_ENC 1024      // single key: 4 waves/SIMD, 128 VGPRs
 #endif
@@ -1968,9 +1971,14 @@ hipError_t launch_decrypt(const DecArgs &args, int nr, int n_cu, SpareQueue *spa
     DecArgs a = args;
     if (!a.ilv && plan_decrypt(a.n, a.tok_len != nullptr, a.uni_len, a.key_idx != nullptr, n_cu) == RT_KERNEL_DEC_LONG2)
         return nr == 14 ? launch_dec_long_nr<14>(a, n_cu, s) : launch_dec_long_nr<10>(a, n_cu, s);
-    // one key and one pass at up to 1024 threads: the 1024-thread instance
+    // one key and one pass at up to 1024 threads: the 1024-thread instance;
+    // so do uniform short tokens (4 waves/SIMD cover the per-token hash tail
+    // and loads, which the 768-thread instance's pairing does not pay for:
+    // 2^20 tokens of 16-250 B plaintext -8..-31 %, 350-430 B +1..+2 %,
+    // profiles/r05r_short/)
     const uint64_t per_cu = ((uint64_t)a.n + n_cu - 1) / n_cu;
-    const int max_t = a.key_idx ? WG_PERKEY_DEC : (per_cu <= 1024u ? 1024 : WG_DEC);
+    const bool short_tok = !a.tok_len && a.uni_len <= RNSTOK_DEC1024_MAX_TOKEN;
+    const int max_t = a.key_idx ? WG_PERKEY_DEC : ((per_cu <= 1024u || short_tok) ? 1024 : WG_DEC);
     const Shape sh = shape_for(a.n, max_t, n_cu);
     bool took = false;
     uint32_t slot = 0;

@@ -1,6 +1,7 @@
 """Large uniform batches on the multi-pass kernels (more than 1 024 tokens per
-CU: the 768-thread single-key decrypt with paired quad loads, the split-role
-encrypt), across lengths that give every tail shape and both parities of
+CU: the 768-thread single-key decrypt with paired quad loads, the 1024-thread
+instance that uniform tokens of at most 320 B take since round 5, the
+split-role encrypt), across lengths that give every tail shape and both parities of
 the quad count: tokens against the C oracle (Token.encrypt, Token.py:87-97)
 on a sample, 1 % of them tampered and a few forged with a bad pad byte,
 decrypt statuses, lengths and plaintexts exactly where the oracle

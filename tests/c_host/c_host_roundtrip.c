@@ -218,6 +218,62 @@ static void interface_path(rt_ctx *c, rt_keyset *ks, const uint8_t *key) {
     free(st); free(ist); free(olen); free(toff); free(ifo); free(back); free(un); free(ref);
 }
 
+/* The measurement and copy helpers from C: rt_clock_stamps around one encrypt
+ * and one decrypt launch (one launch counted each, spans and a plausible shader
+ * clock), and rt_memcpy_d2h_upto with the count read on the device (clamped
+ * to the destination, zero and negative counts copy nothing). */
+static void clock_and_copies(rt_ctx *c, rt_keyset *k1) {
+    enum { M = 1 << 16, L = 500 };
+    const uint32_t tl = (uint32_t)rt_token_len(L);
+    uint8_t *pt = malloc((uint64_t)M * L), *iv = malloc(16 * M);
+    fill(pt, (uint64_t)M * L);
+    fill(iv, 16 * M);
+    uint64_t zero8[RT_CLOCK_WORDS] = {0};
+    uint8_t *d_pt = h2d(c, pt, (uint64_t)M * L), *d_iv = h2d(c, iv, 16 * M);
+    uint8_t *d_tok = dalloc(c, (uint64_t)M * tl), *d_back = dalloc(c, (uint64_t)M * (tl - 48));
+    uint32_t *d_ol = dalloc(c, 4 * M);
+    int32_t *d_st = dalloc(c, 4 * M);
+    uint64_t *d_acc = h2d(c, zero8, sizeof zero8);
+    CHECK(rt_clock_stamps(c, zero8) < 0, "rt_clock_stamps accepted host memory");
+    RT(rt_clock_stamps(c, d_acc));
+    RT(rt_encrypt_uniform(k1, d_pt, L, L, NULL, d_iv, d_tok, tl, M, NULL));
+    RT(rt_decrypt_uniform(k1, d_tok, tl, tl, NULL, d_back, tl - 48, d_ol, d_st, M, NULL));
+    RT(rt_clock_stamps(c, NULL));
+    RT(rt_encrypt_uniform(k1, d_pt, L, L, NULL, d_iv, d_tok, tl, M, NULL));       /* not stamped */
+    uint64_t w[RT_CLOCK_WORDS];
+    d2h(c, w, d_acc, sizeof w);
+    for (int k = RT_CLOCK_ENCRYPT; k <= RT_CLOCK_DECRYPT; ++k) {
+        const uint64_t *x = w + 4 * k;
+        CHECK(x[3] == 1 && x[2] >= 1 && x[0] > 0 && x[1] > 0, "clock words %d: %llu %llu %llu %llu", k,
+              (unsigned long long)x[0], (unsigned long long)x[1], (unsigned long long)x[2], (unsigned long long)x[3]);
+        const double ghz = (double)x[0] / (double)x[1] * 0.1;      /* ticks of 100 MHz */
+        CHECK(ghz > 0.5 && ghz < 2.6, "stamped clock %.3f GHz", ghz);
+    }
+    /* device-sized copies into pinned memory */
+    const uint64_t bytes = (uint64_t)M * (tl - 48);
+    uint8_t *host = rt_host_alloc(bytes + 64), *ref = malloc(bytes);
+    CHECK(host != NULL, "rt_host_alloc");
+    d2h(c, ref, d_back, bytes);
+    const int64_t counts[] = {0, 1, 15, 4097, (int64_t)bytes - 3, (int64_t)bytes + 100, -5};
+    int64_t *d_cnt = dalloc(c, 8);
+    for (unsigned t = 0; t < sizeof counts / sizeof counts[0]; ++t) {
+        memset(host, 0xEE, bytes + 64);
+        RT(rt_memcpy_h2d(c, d_cnt, &counts[t], 8, NULL));
+        RT(rt_memcpy_d2h_upto(c, host + 3, d_back, bytes, (const uint64_t *)d_cnt, NULL));
+        RT(rt_stream_sync(c, NULL));
+        const uint64_t k = counts[t] <= 0 ? 0 : ((uint64_t)counts[t] < bytes ? (uint64_t)counts[t] : bytes);
+        CHECK(memcmp(host + 3, ref, k) == 0, "d2h_upto %lld: bytes differ", (long long)counts[t]);
+        for (uint64_t i = 0; i < 3; ++i) CHECK(host[i] == 0xEE, "d2h_upto wrote before dst");
+        for (uint64_t i = 3 + k; i < bytes + 64; ++i)
+            CHECK(host[i] == 0xEE, "d2h_upto %lld wrote byte %llu past the count", (long long)counts[t],
+                  (unsigned long long)(i - 3));
+    }
+    void *bufs[] = {d_pt, d_iv, d_tok, d_back, d_ol, d_st, d_acc, d_cnt};
+    for (unsigned k = 0; k < sizeof bufs / sizeof bufs[0]; ++k) rt_device_free(c, bufs[k]);
+    rt_host_free(host);
+    free(pt); free(iv); free(ref);
+}
+
 int main(void) {
     CHECK(rt_abi_version() == RNSTOK_ABI_VERSION, "ABI version %d", rt_abi_version());
     CHECK(rt_device_count() > 0, "no device");
@@ -231,10 +287,11 @@ int main(void) {
     rt_keyset *k1 = rt_keyset_create(c, keys, 64, 1);
     CHECK(k1 != NULL, "rt_keyset_create");
     interface_path(c, k1, keys);
+    clock_and_copies(c, k1);
     rt_keyset_destroy(k1);
     rt_keyset_destroy(ks);
     rt_destroy(c);
-    printf("c_host ok: %d ragged tokens (host and device entry points), %d packets through the interface path\n", N,
-           NP);
+    printf("c_host ok: %d ragged tokens (host and device entry points), %d packets through the interface path, "
+           "launch clock and device-sized copies\n", N, NP);
     return 0;
 }

@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--keys", type=int, default=1, help="1 = single link key (c2); 65536 = c3")
     ap.add_argument("--pt-stride", type=int, default=0, help="bytes between plaintext rows in HBM (0: packed)")
     ap.add_argument("--tok-stride", type=int, default=0, help="bytes between token rows in HBM (0: packed)")
+    ap.add_argument("--tok-offset", type=int, default=0,
+                    help="byte offset of the first token row in its buffer (with --tok-stride: row alignment)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 disables)")
     ap.add_argument("--cpu-workers", type=int, default=0, help="0 = every CPU this process may run on")
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
@@ -85,6 +87,8 @@ def parse():
                          "(rt_encrypt_interleaved, coalesced, for batches produced on the device in that layout); "
                          "the other layout is timed right after it")
     ap.add_argument("--one-layout", action="store_true", help="time only --layout")
+    ap.add_argument("--no-aligned", dest="aligned", action="store_false",
+                    help="skip the aligned-slot rows measurement (aligned_rows in the line)")
     ap.add_argument("--e2e", action="store_true", default=True, help="also time the PCIe-inclusive path")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false")
     ap.add_argument("--no-node", dest="node", action="store_false",
@@ -266,7 +270,8 @@ def main():
     ps, ts = max(args.pt_stride, L), max(args.tok_stride, tl)
     pt = torch.randint(0, 256, (n, ps), dtype=torch.uint8, device=dev, generator=g)[:, :L]
     iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
-    tok = torch.empty((n, ts), dtype=torch.uint8, device=dev)[:, :tl]
+    to = args.tok_offset
+    tok = torch.empty(n * ts + to, dtype=torch.uint8, device=dev)[to:].as_strided((n, tl), (ts, 1))
     back = torch.empty((n, max(ps, tl - 48)), dtype=torch.uint8, device=dev)[:, :tl - 48]
     out_len = torch.empty(n, dtype=torch.int32, device=dev)
     status = torch.empty(n, dtype=torch.int32, device=dev)
@@ -324,6 +329,32 @@ def main():
     if len(layouts) == 2 and not torch.equal(device.deinterleave(tok_u, tl), tok):
         raise SystemExit("bench: the two layouts' tokens differ")
 
+    # The same packed rows placed in 128-B-aligned slots (token ciphertext and
+    # plaintext rows starting on a cache line): a caller-side layout choice
+    # (DESIGN.md §4.9).  Same kernels, same bytes; timed after the headline.
+    aligned_step = None
+    if args.aligned and not args.one_layout and args.layout == "rows" and ps == L and ts == tl and args.tok_offset == 0:
+        ps_a, ts_a, to_a = -(-L // 128) * 128, -(-tl // 128) * 128, 128 - 16
+        pt_a = torch.empty((n, ps_a), dtype=torch.uint8, device=dev)[:, :L]
+        pt_a.copy_(pt)
+        tok_a = torch.empty(n * ts_a + to_a, dtype=torch.uint8, device=dev)[to_a:].as_strided((n, tl), (ts_a, 1))
+        back_a = torch.empty((n, ps_a), dtype=torch.uint8, device=dev)[:, :tl - 48]
+
+        def aligned_step(ev=None):
+            if ev is not None:
+                ev[0].record(stream)
+            device.encrypt_uniform(ks, pt_a, L, iv, tok_a, key_idx=key_idx, stream=stream)
+            if ev is not None:
+                ev[1].record(stream)
+            device.decrypt_uniform(ks, tok_a, tl, back_a, out_len, status, key_idx=key_idx, stream=stream)
+            if ev is not None:
+                ev[2].record(stream)
+        aligned_step()
+        torch.cuda.synchronize()
+        if not (bool((status == 0).all()) and bool((out_len == L).all()) and torch.equal(back_a[:, :L], pt)
+                and torch.equal(tok_a, tok)):
+            raise SystemExit("bench: round trip failed on the aligned-slot batch")
+
     def timed(step):
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
         clock = device.LaunchClock(dev)      # the timed launches stamp their own clock (rt_clock_stamps)
@@ -359,6 +390,15 @@ def main():
                  "encrypt_ms": e2, "decrypt_ms": d2, "in_run_clock": clk2,
                  "note": "the same packets in the other HBM layout, timed right after the headline in this run "
                          "(same warmup rule); tokens identical to the headline layout's (checked)"}
+    aligned = None
+    if aligned_step is not None:
+        el3, e3, d3, _, _, _, clk3 = timed(aligned_step)
+        aligned = {"value": n * world * args.steps / el3, "ms_per_step": el3 / args.steps * 1e3,
+                   "encrypt_ms": e3, "decrypt_ms": d3, "in_run_clock": clk3,
+                   "row_strides": {"plaintext": ps_a, "token": ts_a, "token_offset": to_a},
+                   "note": "the headline's packed rows copied into 128-B-aligned slots (each token's ciphertext "
+                           "and each plaintext row starts on a cache line); same kernels and bytes, tokens "
+                           "identical (checked); a caller-side layout choice, not the headline (DESIGN.md §4.9)"}
 
     # PCIe-inclusive (host buffers, pinned) rate for DESIGN.md: every rank at
     # once on its own shard, over its own PCIe link (the node's host-origin rate)
@@ -441,7 +481,7 @@ def main():
                                 f"c3: 2^20 x 500 B packets per GPU, {args.keys} per-packet keys")
                    if (n == 1 << 20 and L == 500) else f"{n} x {L} B packets per GPU, {args.keys} key(s)",
                    "packets_per_gpu": n, "plaintext_bytes": L, "token_bytes": tl, "keys": args.keys,
-                   "row_strides": {"plaintext": ps, "token": ts}, "layout": args.layout,
+                   "row_strides": {"plaintext": ps, "token": ts, "token_offset": args.tok_offset}, "layout": args.layout,
                    "layout_note": ("unit-interleaved: 16-B unit u of packet p at 16*(u*n + p) (rt_encrypt_interleaved; "
                                    "coalesced HBM loads across the batch); the packed-row layout's numbers are under "
                                    "other_layout" if args.layout == "interleaved" else
@@ -493,6 +533,7 @@ def main():
         "cpu_baseline": cpu,
         "cpu_openssl": cpu_ssl,
         "other_layout": other,
+        "aligned_rows": aligned,
         "e2e_pcie": e2e,
         "node_pipeline": node,
         "c4_rank_share_8gpu": shard8,

@@ -35,9 +35,22 @@ from .token import KeySet, token_len
 
 HEADER_1_LEN = 19           # flags, hops, destination hash (16), context: Packet.py:178-228
 FRAME_OK = 0                # RT_FRAME_OK (include/rnstok.h)
+LINE = 128                  # L2 line
+# Outbound builds its packets in 128-B-aligned slots with each HEADER_1
+# packet's token ciphertext (packet + 19 + 16 B of IV) starting on a line: the
+# token encrypt and the IFAC mask then fetch fewer lines twice (DESIGN.md §3,
+# "Rows in 128-B-aligned slots"; §4.8).
+CT_PHASE = HEADER_1_LEN + 16
 
 
-def outbound(ks: KeySet, pt, iv, destination_hash, context, ifac, ifac_key, flags=None, hops=None, stream=None):
+def _slot_base(phase):
+    """Byte offset inside a line at which a packet starts so that its byte
+    ``phase`` starts the next line."""
+    return (-phase) % LINE
+
+
+def outbound(ks: KeySet, pt, iv, destination_hash, context, ifac, ifac_key, flags=None, hops=None, stream=None,
+             aligned=True):
     """n DATA packets of one length L, one link key: pt (n, L) uint8, iv (n,
     16), destination_hash (n, 16), context (n,) uint8, flags/hops (n,) uint8
     (default 0: HEADER_1 DATA, hop 0), ifac (n, ifac_size) the access codes
@@ -45,17 +58,23 @@ def outbound(ks: KeySet, pt, iv, destination_hash, context, ifac, ifac_key, flag
     the caller; None or zero columns: an interface without IFAC, no mask),
     ifac_key (K,) uint8 (unused without IFAC).  Returns (stream, frame_off): the HDLC
     byte stream is stream[:frame_off[n]] (int64 on the device), frame i at
-    stream[frame_off[i]:frame_off[i+1]]."""
+    stream[frame_off[i]:frame_off[i+1]].  ``aligned`` (default) builds the
+    packets in 128-B-aligned slots (token ciphertext on a line); False packs
+    them end to end.  The stream is the same either way."""
     with _on(stream):      # temporaries allocated on the stream that uses them
         n, L = pt.shape
         dev = pt.device
         flags = flags if flags is not None else torch.zeros(n, dtype=torch.uint8, device=dev)
         hops = hops if hops is not None else torch.zeros(n, dtype=torch.uint8, device=dev)
         pl = HEADER_1_LEN + token_len(L)
-        raw = torch.empty((n, pl), dtype=torch.uint8, device=dev)
+        if aligned:
+            stride, base = -(-pl // LINE) * LINE, _slot_base(CT_PHASE)
+        else:
+            stride, base = pl, 0
+        flat = torch.empty(n * stride + base, dtype=torch.uint8, device=dev)[base:]
+        raw = flat.as_strided((n, pl), (stride, 1))
         device.encrypt_uniform(ks, pt, L, iv, raw[:, HEADER_1_LEN:], stream=stream)
-        off = torch.arange(n, dtype=torch.int64, device=dev) * pl
-        flat = raw.view(-1)
+        off = torch.arange(n, dtype=torch.int64, device=dev) * stride
         device.pack_headers(flags, hops, destination_hash, context, flat, off, stream=stream)
         isz = ifac.shape[1] if ifac is not None else 0
         if isz:
@@ -75,7 +94,7 @@ def outbound(ks: KeySet, pt, iv, destination_hash, context, ifac, ifac_key, flag
     return framed, frame_off
 
 
-def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stream=None):
+def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stream=None, aligned=False):
     """One read of an interface's byte stream ``buf`` (uint8 on the device)
     through deframing, IFAC unmask (skipped for ``ifac_size`` 0, an interface
     without access codes: then frames with the IFAC flag set are dropped, as
@@ -96,7 +115,13 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
     outcome: ``status`` (RT_* token status; TOO_SHORT where there is no
     packet) with the plaintext at ``pt[pt_off[i]: pt_off[i] + pt_len[i]]``.
     Compacting first keeps the per-packet kernels' waves full (the gaps
-    between frames would otherwise be half of every wave)."""
+    between frames would otherwise be half of every wave).  With IFAC and
+    ``aligned`` the unmasked packets are written into 128-B-aligned slots (a
+    HEADER_1 packet's token ciphertext on a line, 128 B more buffer per pair)
+    and each plaintext starts on a line too; the default keeps them at their
+    stream offsets, which measured faster end to end (the decrypt gains 5 %,
+    the unmask writing into the slots loses more: DESIGN.md §4.8).  Only the
+    offsets differ."""
     with _on(stream):      # temporaries allocated on the stream that uses them
         dev = buf.device
         # (at least one byte: an empty read still gives every later stage a
@@ -114,12 +139,25 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
         n_frames = torch.empty((), dtype=torch.int64, device=dev)
         device.frames_compact(d_off, d_len, d_st, counts, f_off, f_len, frame_pair, n_frames, stream=stream)
         ifac = torch.empty((max_pairs, ifac_size), dtype=torch.uint8, device=dev)
+        pt_shift = 0
         if ifac_size:
-            un = torch.empty_like(out)
             ifac_status = torch.empty(max_pairs, dtype=torch.int32, device=dev)
             p_len = torch.empty(max_pairs, dtype=torch.int32, device=dev)
-            device.ifac_unmask(out, f_off, f_len, ifac_key, ifac, un, f_off, ifac_status, out_len=p_len,
+            if aligned:
+                # slot i at the first offset >= f_off[i] + 128 i with the
+                # ciphertext phase; slots never overlap since frames do not
+                # (f_off[i+1] >= f_off[i] + f_len[i]) and each slot moves < 128 B
+                base = _slot_base(CT_PHASE)
+                u_off = f_off + torch.arange(max_pairs, dtype=torch.int64, device=dev) * LINE
+                u_off += (base - u_off) % LINE
+                un = torch.empty(out.numel() + LINE * (max_pairs + 1), dtype=torch.uint8, device=dev)
+                pt_shift = 16                 # plaintext i at its token + 16: on a line as well
+            else:
+                u_off = f_off
+                un = torch.empty_like(out)
+            device.ifac_unmask(out, f_off, f_len, ifac_key, ifac, un, u_off, ifac_status, out_len=p_len,
                                stream=stream)
+            f_off = u_off
         else:
             # no IFAC on the interface: a packet with the IFAC flag set is
             # dropped, the others go to unpack as they are
@@ -142,8 +180,9 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
         pt_len = torch.empty(max_pairs, dtype=torch.int32, device=dev)
         status = torch.empty(max_pairs, dtype=torch.int32, device=dev)
         # each plaintext (at most its token's length - 48 bytes) is written inside its own token's span
-        device.decrypt(ks, un, tok_off, tok_len, pt, tok_off, pt_len, status, stream=stream)
-    return {"pt": pt, "pt_off": tok_off, "pt_len": pt_len, "status": status, "ifac": ifac,
+        pt_off = tok_off + pt_shift if pt_shift else tok_off
+        device.decrypt(ks, un, tok_off, tok_len, pt, pt_off, pt_len, status, stream=stream)
+    return {"pt": pt, "pt_off": pt_off, "pt_len": pt_len, "status": status, "ifac": ifac,
             "ifac_status": ifac_status, "fields": fields, "frame_pair": frame_pair, "n_frames": n_frames,
             "frame_status": d_st, "frame_len": d_len, "counts": counts}
 

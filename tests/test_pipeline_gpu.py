@@ -117,3 +117,36 @@ def test_pipeline_on_a_side_stream_matches_default_stream():
     po = ref0["pt_off"][:n].cpu().numpy()
     p0, p1 = ref0["pt"].cpu().numpy(), res1["pt"].cpu().numpy()
     assert all((p0[o:o + L] == p1[o:o + L]).all() for o in po)
+
+
+@pytest.mark.parametrize("n,L,isz", [(1500, 383, 16), (700, 17, 8), (257, 0, 32)])
+def test_aligned_slots_change_only_offsets(n, L, isz):
+    """The pipeline's own packet buffers in 128-B-aligned slots (the default,
+    DESIGN.md §3) against packets packed end to end: the same HDLC stream, and
+    inbound the same frames, IFACs, header fields, statuses and plaintexts;
+    with slots every plaintext (and so every token's ciphertext) starts on a
+    128-B line of its buffer."""
+    import torch
+    import reticulum_amd as rt
+    from reticulum_amd import pipeline
+    key, ifac_key, pt, iv, dh, ctx, ifac, t = _case(n, L, isz, 900 + n + L)
+    ks = rt.KeySet(key, device=0)
+    args = (t(pt), t(iv), t(dh), t(ctx), t(ifac), t(np.frombuffer(ifac_key, np.uint8)))
+    fa, oa = pipeline.outbound(ks, *args, aligned=True)
+    fp, op = pipeline.outbound(ks, *args, aligned=False)
+    total = int(oa[-1])
+    assert torch.equal(oa, op) and torch.equal(fa[:total], fp[:total])
+    buf = fa[:total].clone()
+    ra = pipeline.inbound(ks, buf, args[5], isz, 2 * n, aligned=True)
+    rp = pipeline.inbound(ks, buf, args[5], isz, 2 * n, aligned=False)
+    torch.cuda.synchronize()
+    for k in ("status", "pt_len", "frame_pair", "ifac_status", "n_frames", "counts", "frame_status"):
+        assert torch.equal(ra[k], rp[k]), k
+    assert torch.equal(ra["frame_len"][:2 * n - 1], rp["frame_len"][:2 * n - 1])    # past the pairs: unspecified
+    assert torch.equal(ra["ifac"][:n], rp["ifac"][:n]) and torch.equal(ra["fields"][:n], rp["fields"][:n])
+    assert bool((ra["status"][:n] == 0).all())
+    poa, pop = ra["pt_off"][:n].cpu().numpy(), rp["pt_off"][:n].cpu().numpy()
+    assert ((ra["pt"].data_ptr() + poa) % 128 == 0).all()
+    pa, pp = ra["pt"].cpu().numpy(), rp["pt"].cpu().numpy()
+    for i in range(n):
+        assert pa[poa[i]:poa[i] + L].tobytes() == pp[pop[i]:pop[i] + L].tobytes() == pt[i].tobytes(), i

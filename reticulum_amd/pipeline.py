@@ -67,6 +67,7 @@ def outbound(ks: KeySet, pt, iv, destination_hash, context, ifac, ifac_key, flag
         flags = flags if flags is not None else torch.zeros(n, dtype=torch.uint8, device=dev)
         hops = hops if hops is not None else torch.zeros(n, dtype=torch.uint8, device=dev)
         pl = HEADER_1_LEN + token_len(L)
+        isz = ifac.shape[1] if ifac is not None else 0
         if aligned:
             stride, base = -(-pl // LINE) * LINE, _slot_base(CT_PHASE)
         else:
@@ -76,7 +77,6 @@ def outbound(ks: KeySet, pt, iv, destination_hash, context, ifac, ifac_key, flag
         device.encrypt_uniform(ks, pt, L, iv, raw[:, HEADER_1_LEN:], stream=stream)
         off = torch.arange(n, dtype=torch.int64, device=dev) * stride
         device.pack_headers(flags, hops, destination_hash, context, flat, off, stream=stream)
-        isz = ifac.shape[1] if ifac is not None else 0
         if isz:
             ml = pl + isz
             masked = torch.empty(n * ml, dtype=torch.uint8, device=dev)

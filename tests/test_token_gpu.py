@@ -512,6 +512,41 @@ def test_device_uniform_row_views(rt):
         device.encrypt_uniform(ks, wide[:, ::2], 256, iv, tok_a)       # bytes of a row not contiguous
 
 
+@pytest.mark.parametrize("n,L", [(5000, 500), (300_000, 500), (70_000, 1500)])
+def test_device_uniform_aligned_slots(rt, n, L):
+    """Rows in 128-B-aligned slots as INTEGRATION.md §3 recommends them (a
+    token buffer whose first row starts 112 B in, so every ciphertext starts
+    on a line; plaintext rows at a multiple-of-128 stride): the same tokens
+    and plaintexts as packed rows, the bytes between slots untouched, at a
+    one-pass, a multi-pass and a long-packet size."""
+    import torch
+    from reticulum_amd import device
+    tl = rt.token_len(L)
+    ps, ts, to = -(-L // 128) * 128, -(-tl // 128) * 128, 112
+    g = torch.Generator(device="cuda").manual_seed(n + L)
+    pt = torch.randint(0, 256, (n, L), dtype=torch.uint8, device="cuda", generator=g)
+    iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
+    ks = rt.KeySet(bytes(range(64)))
+    tok_p = torch.empty((n, tl), dtype=torch.uint8, device="cuda")
+    device.encrypt_uniform(ks, pt, L, iv, tok_p)
+    pt_s = torch.zeros((n, ps), dtype=torch.uint8, device="cuda")
+    pt_s[:, :L] = pt
+    buf = torch.zeros(n * ts + to, dtype=torch.uint8, device="cuda")
+    tok_s = buf[to:].as_strided((n, tl), (ts, 1))
+    assert (tok_s.data_ptr() + 16) % 128 == 0
+    device.encrypt_uniform(ks, pt_s[:, :L], L, iv, tok_s)
+    back = torch.zeros((n, ps), dtype=torch.uint8, device="cuda")
+    ol = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    device.decrypt_uniform(ks, tok_s, tl, back[:, :tl - 48], ol, st)
+    torch.cuda.synchronize()
+    assert torch.equal(tok_s, tok_p)
+    assert int(buf[:to].count_nonzero()) == 0
+    assert int(buf[to:].view(n, ts)[:, tl:].count_nonzero()) == 0       # bytes between slots untouched
+    assert int(st.abs().sum()) == 0 and bool((ol == L).all()) and torch.equal(back[:, :L], pt)
+    assert int(back[:, tl - 48:].count_nonzero()) == 0
+
+
 def test_verify_trials_vs_oracle(rt):
     """Ratchet trials (Identity.py:865-878) on the GPU: the first candidate
     key that opens each token (right key at a random rank, missing, twice;

@@ -338,7 +338,7 @@ def main():
         pt_a = torch.empty((n, ps_a), dtype=torch.uint8, device=dev)[:, :L]
         pt_a.copy_(pt)
         tok_a = torch.empty(n * ts_a + to_a, dtype=torch.uint8, device=dev)[to_a:].as_strided((n, tl), (ts_a, 1))
-        back_a = torch.empty((n, ps_a), dtype=torch.uint8, device=dev)[:, :tl - 48]
+        back_a = torch.empty((n, -(-(tl - 48) // 128) * 128), dtype=torch.uint8, device=dev)[:, :tl - 48]
 
         def aligned_step(ev=None):
             if ev is not None:

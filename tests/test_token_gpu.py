@@ -512,7 +512,7 @@ def test_device_uniform_row_views(rt):
         device.encrypt_uniform(ks, wide[:, ::2], 256, iv, tok_a)       # bytes of a row not contiguous
 
 
-@pytest.mark.parametrize("n,L", [(5000, 500), (300_000, 500), (70_000, 1500)])
+@pytest.mark.parametrize("n,L", [(5000, 500), (300_000, 500), (70_000, 1500), (9000, 128)])
 def test_device_uniform_aligned_slots(rt, n, L):
     """Rows in 128-B-aligned slots as INTEGRATION.md §3 recommends them (a
     token buffer whose first row starts 112 B in, so every ciphertext starts
@@ -535,7 +535,7 @@ def test_device_uniform_aligned_slots(rt, n, L):
     tok_s = buf[to:].as_strided((n, tl), (ts, 1))
     assert (tok_s.data_ptr() + 16) % 128 == 0
     device.encrypt_uniform(ks, pt_s[:, :L], L, iv, tok_s)
-    back = torch.zeros((n, ps), dtype=torch.uint8, device="cuda")
+    back = torch.zeros((n, -(-(tl - 48) // 128) * 128), dtype=torch.uint8, device="cuda")
     ol = torch.empty(n, dtype=torch.int32, device="cuda")
     st = torch.empty(n, dtype=torch.int32, device="cuda")
     device.decrypt_uniform(ks, tok_s, tl, back[:, :tl - 48], ol, st)

@@ -88,3 +88,56 @@ def test_multipass_uniform_batches_vs_oracle(rt, L, klen, nk):
     ok = st_h == 0
     assert (ol_h[ok] == L).all()
     assert np.array_equal(b_h[ok, :L], p_h[ok])
+
+
+@pytest.mark.parametrize("nk,sort", [(1, True), (97, False)])
+def test_packed_offsets_past_4gib(rt, nk, sort):
+    """Packed batches whose offsets cross 2^32: 200 000 packets of 0-600 B laid
+    end to end from 40 MB below the 4 GiB mark in 4.3-GB plaintext and token
+    buffers (unaligned), sorted by length (the split kernel's packed instance)
+    or not, one key or per-packet keys: every packet round-trips and a sample
+    spanning the boundary matches the oracle."""
+    import torch
+    from reticulum_amd import device
+    n = 200_000
+    rng = np.random.Generator(np.random.PCG64(4242 + nk))
+    L = rng.integers(0, 601, n).astype(np.int64)
+    T = 16 + 16 * (L // 16 + 1) + 32
+    start = (1 << 32) - 40_000_003
+    po = start + np.concatenate(([0], np.cumsum(L)[:-1]))
+    to = start + 7 + np.concatenate(([0], np.cumsum(T)[:-1]))
+    assert po[-1] > (1 << 32) and to[-1] > (1 << 32)
+    dev = torch.device("cuda")
+    pt = torch.empty(int(po[-1] + L[-1]) + 1, dtype=torch.uint8, device=dev)
+    pt[start:].random_(0, 256, generator=torch.Generator(device=dev).manual_seed(nk))
+    keys = rng.integers(0, 256, (nk, 64), dtype=np.uint8)
+    ks = rt.KeySet(keys)
+    ki = torch.from_numpy(rng.integers(0, nk, n).astype(np.int32)).to(dev) if nk > 1 else None
+    iv = torch.from_numpy(rng.integers(0, 256, (n, 16), dtype=np.uint8)).to(dev)
+    tok = torch.zeros(int(to[-1] + T[-1]) + 1, dtype=torch.uint8, device=dev)
+    t_po, t_to = torch.from_numpy(po).to(dev), torch.from_numpy(to).to(dev)
+    t_L, t_T = torch.from_numpy(L.astype(np.int32)).to(dev), torch.from_numpy(T.astype(np.int32)).to(dev)
+    device.encrypt(ks, pt, t_po, t_L, iv, tok, t_to, key_idx=ki, sort=sort)
+    # plaintexts back at their own offsets, each with room for its pad block
+    bo = start + 5 + np.concatenate(([0], np.cumsum(T - 48)[:-1]))
+    back = torch.zeros(int(bo[-1] + T[-1] - 48) + 1, dtype=torch.uint8, device=dev)
+    t_bo = torch.from_numpy(bo).to(dev)
+    ol = torch.empty(n, dtype=torch.int32, device=dev)
+    st = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    device.decrypt(ks, tok, t_to, t_T, back, t_bo, ol, st, key_idx=ki, sort=sort)
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0 and torch.equal(ol.cpu(), t_L.cpu())
+    # every plaintext byte, gathered on the device
+    tl64 = t_L.to(torch.int64)
+    first = torch.repeat_interleave(torch.cumsum(tl64, 0) - tl64, tl64)
+    k = torch.arange(int(L.sum()), device=dev) - first
+    assert torch.equal(back[torch.repeat_interleave(t_bo, tl64) + k], pt[torch.repeat_interleave(t_po, tl64) + k])
+    cross = int(np.searchsorted(po, 1 << 32))
+    sel = np.unique(np.concatenate([np.arange(max(cross - 40, 0), min(cross + 40, n)),
+                                    rng.choice(n, 120, replace=False)]))
+    kih = ki.cpu().numpy() if ki is not None else np.zeros(n, np.int32)
+    ivh = iv.cpu().numpy()
+    for i in sel:
+        p = pt[int(po[i]):int(po[i] + L[i])].cpu().numpy().tobytes()
+        ref = oracle.encrypt(keys[kih[i]].tobytes(), ivh[i].tobytes(), p)
+        assert tok[int(to[i]):int(to[i] + T[i])].cpu().numpy().tobytes() == ref, int(i)

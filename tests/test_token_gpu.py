@@ -360,7 +360,9 @@ def test_sorted_small_batches_chunk_edges(rt, n, n_keys, klen):
                                        # short packets take the single-key long kernels too (round 2)
                                        (1, 0, 64), (1, 15, 64), (3, 16, 64), (129, 17, 64), (300, 100, 32),
                                        (1, 500, 64), (64, 500, 64), (32768, 500, 64), (257, 63, 64),
-                                       (5, 1023, 32), (2, 47, 32), (200, 48, 64)])
+                                       (5, 1023, 32), (2, 47, 32), (200, 48, 64),
+                                       # one multi-MiB token (no length limit in Token.py)
+                                       (1, 4_194_309, 64), (3, 1_000_003, 32)])
 def test_long_token_mode_vs_oracle(rt, n, L, klen):
     """Uniform batches of long tokens with few packets per CU take the
     long-token kernels (single key: a quad of lanes per CBC chain, AES waves

@@ -100,7 +100,10 @@ def test_gpu_hkdf_golden(golden_hkdf):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("salt_len,ctx_len,length", [(16, 0, 64), (0, 0, 32), (100, 30, 200), (64, 1, 33),
-                                                    (64, 0, 64), (20, 0, 100), (18, 0, 64)])
+                                                    (64, 0, 64), (20, 0, 100), (18, 0, 64),
+                                                    # the longest output HKDF allows (255 blocks), a context
+                                                    # longer than a block
+                                                    (16, 0, 8160), (0, 100, 8160), (32, 200, 96)])
 def test_gpu_hkdf_device_batch_vs_oracle(salt_len, ctx_len, length):
     import torch
     from reticulum_amd import device

@@ -334,11 +334,11 @@ def main():
     # (DESIGN.md §4.9).  Same kernels, same bytes; timed after the headline.
     aligned_step = None
     if args.aligned and not args.one_layout and args.layout == "rows" and ps == L and ts == tl and args.tok_offset == 0:
-        ps_a, ts_a, to_a = -(-L // 128) * 128, -(-tl // 128) * 128, 128 - 16
-        pt_a = torch.empty((n, ps_a), dtype=torch.uint8, device=dev)[:, :L]
+        pt_a = device.aligned_rows(n, L, 0, dev)          # plaintext rows on lines
         pt_a.copy_(pt)
-        tok_a = torch.empty(n * ts_a + to_a, dtype=torch.uint8, device=dev)[to_a:].as_strided((n, tl), (ts_a, 1))
-        back_a = torch.empty((n, -(-(tl - 48) // 128) * 128), dtype=torch.uint8, device=dev)[:, :tl - 48]
+        tok_a = device.aligned_rows(n, tl, 16, dev)       # each token's ciphertext on a line
+        back_a = device.aligned_rows(n, tl - 48, 0, dev)
+        ps_a, ts_a, to_a = pt_a.stride(0), tok_a.stride(0), 128 - 16
 
         def aligned_step(ev=None):
             if ev is not None:
@@ -395,7 +395,7 @@ def main():
         el3, e3, d3, _, _, _, clk3 = timed(aligned_step)
         aligned = {"value": n * world * args.steps / el3, "ms_per_step": el3 / args.steps * 1e3,
                    "encrypt_ms": e3, "decrypt_ms": d3, "in_run_clock": clk3,
-                   "row_strides": {"plaintext": ps_a, "token": ts_a, "token_offset": to_a},
+                   "row_strides": {"plaintext": ps_a, "token": ts_a, "token_line_offset": to_a},
                    "note": "the headline's packed rows copied into 128-B-aligned slots (each token's ciphertext "
                            "and each plaintext row starts on a cache line); same kernels and bytes, tokens "
                            "identical (checked); a caller-side layout choice, not the headline (DESIGN.md §4.9)"}

@@ -45,7 +45,8 @@ CT_PHASE = HEADER_1_LEN + 16
 
 def _slot_base(phase):
     """Byte offset inside a line at which a packet starts so that its byte
-    ``phase`` starts the next line."""
+    ``phase`` starts the next line (for a buffer that starts on a line; with
+    phase = (data_ptr + phase) % 128, for any buffer)."""
     return (-phase) % LINE
 
 
@@ -69,11 +70,13 @@ def outbound(ks: KeySet, pt, iv, destination_hash, context, ifac, ifac_key, flag
         pl = HEADER_1_LEN + token_len(L)
         isz = ifac.shape[1] if ifac is not None else 0
         if aligned:
-            stride, base = -(-pl // LINE) * LINE, _slot_base(CT_PHASE)
+            raw = device.aligned_rows(n, pl, CT_PHASE, dev)
+            stride = raw.stride(0)
+            flat = raw.as_strided((n * stride,), (1,))
         else:
-            stride, base = pl, 0
-        flat = torch.empty(n * stride + base, dtype=torch.uint8, device=dev)[base:]
-        raw = flat.as_strided((n, pl), (stride, 1))
+            stride = pl
+            flat = torch.empty(n * stride, dtype=torch.uint8, device=dev)
+            raw = flat.view(n, pl)
         device.encrypt_uniform(ks, pt, L, iv, raw[:, HEADER_1_LEN:], stream=stream)
         off = torch.arange(n, dtype=torch.int64, device=dev) * stride
         device.pack_headers(flags, hops, destination_hash, context, flat, off, stream=stream)
@@ -147,10 +150,10 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
                 # slot i at the first offset >= f_off[i] + 128 i with the
                 # ciphertext phase; slots never overlap since frames do not
                 # (f_off[i+1] >= f_off[i] + f_len[i]) and each slot moves < 128 B
-                base = _slot_base(CT_PHASE)
+                un = torch.empty(out.numel() + LINE * (max_pairs + 1), dtype=torch.uint8, device=dev)
+                base = _slot_base((un.data_ptr() + CT_PHASE) % LINE)
                 u_off = f_off + torch.arange(max_pairs, dtype=torch.int64, device=dev) * LINE
                 u_off += (base - u_off) % LINE
-                un = torch.empty(out.numel() + LINE * (max_pairs + 1), dtype=torch.uint8, device=dev)
                 pt_shift = 16                 # plaintext i at its token + 16: on a line as well
             else:
                 u_off = f_off

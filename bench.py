@@ -1222,7 +1222,9 @@ def node_host_rate(dev, n=1 << 20, L=383, isz=16, slices=32, n_streams=3, reps=3
             lo, hi = int(fo[a]), int(fo[b])
             with torch.cuda.stream(s):
                 stream_d[lo:hi].copy_(stream_h[lo:hi], non_blocking=True)
-                r = pipeline.inbound(ks, stream_d[lo:hi], ikey, isz, 2 * (b - a), stream=s)
+                # stream offsets, not slots: the plaintext buffer crosses PCIe
+                # whole, and slots would add 256 B per packet to it
+                r = pipeline.inbound(ks, stream_d[lo:hi], ikey, isz, 2 * (b - a), stream=s, aligned=False)
                 device.copy_to_host(pt_h[lo:hi], r["pt"], stream=s)
                 m = torch.stack([r["pt_off"][:b - a], r["pt_len"][:b - a].to(torch.int64),
                                  r["status"][:b - a].to(torch.int64)])

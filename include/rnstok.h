@@ -20,6 +20,7 @@
  *                                                receive_part :865-866
  *   rt_hdlc_frame      HDLC.escape + framing     RNS/Interfaces/TCPInterface.py:44-53, :323
  *   rt_hdlc_deframe    HDLC read loop            RNS/Interfaces/TCPInterface.py:387-410, :336-339
+ *   rt_hdlc_deframe_slots  the same, each frame in a 128-B-aligned slot
  *   rt_ifac_mask       IFAC on transmit          RNS/Transport.py:1069-1101
  *   rt_ifac_unmask     IFAC on inbound           RNS/Transport.py:1441-1475
  *   rt_packet_unpack   Packet.unpack + get_hash  RNS/Packet.py:236-268, 342-353
@@ -314,6 +315,18 @@ uint64_t rt_hdlc_deframe_workspace_bytes(uint64_t len);
 int rt_hdlc_deframe(rt_ctx *ctx, const uint8_t *buf, uint64_t len, uint32_t hw_mtu, uint32_t ifac_size, uint8_t *out,
                     uint64_t *frame_off, uint32_t *frame_len, int32_t *status, uint64_t *counts, uint64_t max_pairs,
                     void *workspace, void *stream);
+/* rt_hdlc_deframe with every frame in its own 128-B-aligned slot instead of
+ * at its position in buf: frame k is written at the first offset >=
+ * pos_k + 1 + 128*k (pos_k: its opening flag) at which byte line_phase (< 128)
+ * of the frame starts a 128-B line of memory, so `out` needs
+ * len + 128 * (max_pairs + 1) bytes.  Frame bytes, lengths, statuses and
+ * counts are those of rt_hdlc_deframe; only frame_off differs.  With
+ * line_phase = 35 a HEADER_1 packet at the frame's offset (as it is, or
+ * IFAC-unmasked into another buffer at the same offset) has its token
+ * ciphertext on a line. */
+int rt_hdlc_deframe_slots(rt_ctx *ctx, const uint8_t *buf, uint64_t len, uint32_t hw_mtu, uint32_t ifac_size,
+                          uint32_t line_phase, uint8_t *out, uint64_t *frame_off, uint32_t *frame_len, int32_t *status,
+                          uint64_t *counts, uint64_t max_pairs, void *workspace, void *stream);
 /* The frames one rt_hdlc_deframe pass hands on (pair k < counts[0] with
  * status[k] == RT_FRAME_OK), in stream order, to the front of f_off / f_len
  * (their offsets and lengths in the deframed buffer) and frame_pair (k);

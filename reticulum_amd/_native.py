@@ -57,6 +57,7 @@ SIGNATURES = [
     ("rt_hdlc_frame", _int, [_vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp]),
     ("rt_hdlc_deframe_workspace_bytes", _u64, [_u64]),
     ("rt_hdlc_deframe", _int, [_vp, _vp, _u64, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp]),
+    ("rt_hdlc_deframe_slots", _int, [_vp, _vp, _u64, _u32, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp]),
     ("rt_ifac_mask", _int, [_vp, _vp, _vp, _vp, _vp, _u32, _vp, _u32, _vp, _vp, _u32, _vp]),
     ("rt_ifac_unmask", _int, [_vp, _vp, _vp, _vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),
     ("rt_packet_unpack", _int, [_vp, _vp, _vp, _vp, _vp, _u32, _vp]),

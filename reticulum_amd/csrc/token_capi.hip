@@ -842,18 +842,33 @@ int rt_hdlc_frame(rt_ctx *c, const uint8_t *pkt, const uint64_t *pkt_off, const 
     return RT_OK;
 }
 
-int rt_hdlc_deframe(rt_ctx *c, const uint8_t *buf, uint64_t len, uint32_t hw_mtu, uint32_t ifac_size, uint8_t *out,
-                    uint64_t *frame_off, uint32_t *frame_len, int32_t *status, uint64_t *counts, uint64_t max_pairs,
-                    void *workspace, void *stream) {
+static int deframe_common(rt_ctx *c, const uint8_t *buf, uint64_t len, uint32_t hw_mtu, uint32_t ifac_size,
+                          uint8_t *out, uint64_t *frame_off, uint32_t *frame_len, int32_t *status, uint64_t *counts,
+                          uint64_t max_pairs, void *workspace, void *stream, uint32_t line_phase) {
     if (!c) return fail(RT_E_INVAL, "null context");
     if (!counts || !workspace) return fail(RT_E_INVAL, "rt_hdlc_deframe: null counts/workspace");
     if (len && (!buf || !out)) return fail(RT_E_INVAL, "rt_hdlc_deframe: null buffer");
     if (max_pairs && (!frame_off || !frame_len || !status)) return fail(RT_E_INVAL, "rt_hdlc_deframe: null frame arrays");
     RT_HIP(hipSetDevice(c->device), "hipSetDevice");
     RT_HIP(launch_hdlc_deframe(buf, len, hw_mtu, ifac_size, out, frame_off, frame_len, status, counts, max_pairs,
-                               workspace, pick(c, stream)),
+                               workspace, pick(c, stream), line_phase),
            "hdlc deframe");
     return RT_OK;
+}
+
+int rt_hdlc_deframe(rt_ctx *c, const uint8_t *buf, uint64_t len, uint32_t hw_mtu, uint32_t ifac_size, uint8_t *out,
+                    uint64_t *frame_off, uint32_t *frame_len, int32_t *status, uint64_t *counts, uint64_t max_pairs,
+                    void *workspace, void *stream) {
+    return deframe_common(c, buf, len, hw_mtu, ifac_size, out, frame_off, frame_len, status, counts, max_pairs,
+                          workspace, stream, 0xFFFFFFFFu);
+}
+
+int rt_hdlc_deframe_slots(rt_ctx *c, const uint8_t *buf, uint64_t len, uint32_t hw_mtu, uint32_t ifac_size,
+                          uint32_t line_phase, uint8_t *out, uint64_t *frame_off, uint32_t *frame_len, int32_t *status,
+                          uint64_t *counts, uint64_t max_pairs, void *workspace, void *stream) {
+    if (line_phase >= 128u) return fail(RT_E_INVAL, "rt_hdlc_deframe_slots: line_phase must be < 128");
+    return deframe_common(c, buf, len, hw_mtu, ifac_size, out, frame_off, frame_len, status, counts, max_pairs,
+                          workspace, stream, line_phase);
 }
 
 static bool overlaps(const void *a, const void *b, uint64_t a_bytes, uint64_t b_bytes = 0) {

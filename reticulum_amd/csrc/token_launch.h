@@ -127,7 +127,7 @@ hipError_t launch_hdlc_frame(const uint8_t *pkt, const uint64_t *off, const uint
                              uint64_t *frame_off, void *ws, hipStream_t s);
 hipError_t launch_hdlc_deframe(const uint8_t *buf, uint64_t len, uint32_t hw_mtu, uint32_t ifac_size, uint8_t *out,
                                uint64_t *frame_off, uint32_t *frame_len, int32_t *status, uint64_t *counts,
-                               uint64_t max_pairs, void *ws, hipStream_t s);
+                               uint64_t max_pairs, void *ws, hipStream_t s, uint32_t line_phase = 0xFFFFFFFFu);
 hipError_t launch_ifac(const IfacArgs &a, bool mask, hipStream_t s);
 uint64_t frames_compact_workspace_bytes(uint64_t max_pairs);
 hipError_t launch_frames_compact(const uint64_t *d_off, const uint32_t *d_len, const int32_t *st,

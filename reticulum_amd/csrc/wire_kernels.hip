@@ -416,7 +416,8 @@ __device__ void deframe_counts(const uint64_t *nflags_p, const uint64_t *pos, ui
 __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, uint64_t len, const uint64_t *pos,
                                                        const uint64_t *nflags_p, uint64_t max_pairs, uint32_t hw_mtu,
                                                        uint32_t ifac_size, uint8_t *out, uint64_t *frame_off,
-                                                       uint32_t *frame_len, int32_t *status, uint64_t *counts) {
+                                                       uint32_t *frame_len, int32_t *status, uint64_t *counts,
+                                                       uint32_t line_phase) {
     __shared__ SelTables tab;
     // the pair count and the bytes consumed (k_deframe_counts' job, folded in: one launch fewer)
     if (blockIdx.x == 0 && threadIdx.x == 0) deframe_counts(nflags_p, pos, len, hw_mtu, counts);
@@ -436,7 +437,15 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, uint6
         const uint64_t k = 4 * PPR * g + PPR * (lane >> 4) + sub;
         const bool valid = k < npairs;
         const uint64_t a = valid ? pos[k] + 1 : 0, e = valid ? pos[k + 1] : 0;
-        uint8_t *o = out + a;
+        // slots (line_phase < 128): frame k at the first offset >= a + 128 k
+        // whose byte line_phase starts a 128-B line; frames never overlap,
+        // since each moves by less than 128 B more than the one before it
+        uint64_t ao = a;
+        if (line_phase < 128u) {
+            ao = a + 128ull * k;
+            ao += (0ull - ((uint64_t)(uintptr_t)out + ao + line_phase)) & 127ull;
+        }
+        uint8_t *o = out + ao;
         uint64_t kept_total = 0;
         uint32_t carry = FLAG;                    // the byte before the window: the opening flag first
         for (uint64_t w = a; w < e; w += 256u) {
@@ -557,7 +566,7 @@ __global__ __launch_bounds__(256) void k_hdlc_unescape(const uint8_t *buf, uint6
             carry = row_sum16(rl == 15 ? v.w >> 24 : 0u);      // the window's last byte, to every lane
         }
         if (rl == 0 && valid) {
-            frame_off[k] = a;
+            frame_off[k] = ao;
             frame_len[k] = (uint32_t)kept_total;
             // check_frame_len (TCPInterface.py:336-339); empty frames are skipped (:400)
             status[k] = kept_total == 0 ? RT_FRAME_EMPTY
@@ -1010,7 +1019,7 @@ uint64_t hdlc_deframe_workspace_bytes(uint64_t len) {
 
 hipError_t launch_hdlc_deframe(const uint8_t *buf, uint64_t len, uint32_t hw_mtu, uint32_t ifac_size, uint8_t *out,
                                uint64_t *frame_off, uint32_t *frame_len, int32_t *status, uint64_t *counts,
-                               uint64_t max_pairs, void *ws, hipStream_t s) {
+                               uint64_t max_pairs, void *ws, hipStream_t s, uint32_t line_phase) {
     const uint64_t chunks = (len + FLAG_CHUNK - 1) / FLAG_CHUNK;
     uint64_t *cnt = (uint64_t *)ws;
     uint64_t *cnt_off = cnt + chunks;
@@ -1035,7 +1044,7 @@ hipError_t launch_hdlc_deframe(const uint8_t *buf, uint64_t len, uint32_t hw_mtu
     if (max_pairs) {
         const uint64_t g = min((max_pairs + 15) / 16, (uint64_t)WAVE_GRID);   // one DPP row per frame
         hipLaunchKernelGGL(k_hdlc_unescape, dim3((unsigned)g), dim3(256), 0, s, buf, len, pos, nflags, max_pairs,
-                           hw_mtu, ifac_size, out, frame_off, frame_len, status, counts);
+                           hw_mtu, ifac_size, out, frame_off, frame_len, status, counts, line_phase);
     } else {
         hipLaunchKernelGGL(k_deframe_counts, dim3(1), dim3(1), 0, s, nflags, pos, len, hw_mtu, counts);
     }

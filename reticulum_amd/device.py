@@ -389,22 +389,37 @@ def hdlc_frame(pkt, pkt_off, pkt_len, out, frame_off, workspace=None, stream=Non
                                     _p(ws), _stream(stream, pkt.device)))
 
 
+def deframe_slots_bytes(nbytes, max_pairs):
+    """Output capacity hdlc_deframe needs with ``line_phase`` (slots)."""
+    return int(nbytes) + LINE * (int(max_pairs) + 1)
+
+
 def hdlc_deframe(buf, out, frame_off, frame_len, status, counts, hw_mtu=262144, ifac_size=0, workspace=None,
-                 stream=None):
+                 stream=None, line_phase=None):
     """One pass of the HDLC read loop (TCPInterface.py:387-410) over ``buf``:
     for each consecutive flag pair k (at most frame_off.numel() pairs) the
     unescaped frame at out[frame_off[k]: frame_off[k] + frame_len[k]] with its
-    RT_FRAME_* status; counts (2,) int64 = [pairs, bytes consumed]."""
+    RT_FRAME_* status; counts (2,) int64 = [pairs, bytes consumed].  With
+    ``line_phase`` (0..127) each frame gets a 128-B-aligned slot whose byte
+    line_phase starts a line (rt_hdlc_deframe_slots; ``out`` then needs
+    deframe_slots_bytes(len(buf), max_pairs) bytes), else it sits at its
+    position in buf."""
     _check_u8(buf, out)
     max_pairs = frame_off.numel()
-    if frame_len.numel() != max_pairs or status.numel() != max_pairs or counts.numel() < 2 or \
-            out.numel() < buf.numel():
+    need = buf.numel() if line_phase is None else deframe_slots_bytes(buf.numel(), max_pairs)
+    if frame_len.numel() != max_pairs or status.numel() != max_pairs or counts.numel() < 2 or out.numel() < need:
         raise ValueError("shape mismatch")
     lib = _native.load()
     ws = workspace if workspace is not None else torch.empty(
         int(lib.rt_hdlc_deframe_workspace_bytes(buf.numel())), dtype=torch.uint8, device=buf.device)
-    _native.check(lib.rt_hdlc_deframe(_ctx_of(buf), _p(buf), buf.numel(), hw_mtu, ifac_size, _p(out), _p(frame_off),
-                                      _p(frame_len), _p(status), _p(counts), max_pairs, _p(ws), _stream(stream, buf.device)))
+    if line_phase is None:
+        _native.check(lib.rt_hdlc_deframe(_ctx_of(buf), _p(buf), buf.numel(), hw_mtu, ifac_size, _p(out),
+                                          _p(frame_off), _p(frame_len), _p(status), _p(counts), max_pairs, _p(ws),
+                                          _stream(stream, buf.device)))
+    else:
+        _native.check(lib.rt_hdlc_deframe_slots(_ctx_of(buf), _p(buf), buf.numel(), hw_mtu, ifac_size, int(line_phase),
+                                                _p(out), _p(frame_off), _p(frame_len), _p(status), _p(counts),
+                                                max_pairs, _p(ws), _stream(stream, buf.device)))
 
 
 def frames_compact(frame_off, frame_len, status, counts, f_off, f_len, frame_pair, n_frames, workspace=None,

@@ -35,19 +35,11 @@ from .token import KeySet, token_len
 
 HEADER_1_LEN = 19           # flags, hops, destination hash (16), context: Packet.py:178-228
 FRAME_OK = 0                # RT_FRAME_OK (include/rnstok.h)
-LINE = 128                  # L2 line
 # Outbound builds its packets in 128-B-aligned slots with each HEADER_1
 # packet's token ciphertext (packet + 19 + 16 B of IV) starting on a line: the
 # token encrypt and the IFAC mask then fetch fewer lines twice (DESIGN.md §3,
 # "Rows in 128-B-aligned slots"; §4.8).
 CT_PHASE = HEADER_1_LEN + 16
-
-
-def _slot_base(phase):
-    """Byte offset inside a line at which a packet starts so that its byte
-    ``phase`` starts the next line (for a buffer that starts on a line; with
-    phase = (data_ptr + phase) % 128, for any buffer)."""
-    return (-phase) % LINE
 
 
 def outbound(ks: KeySet, pt, iv, destination_hash, context, ifac, ifac_key, flags=None, hops=None, stream=None,
@@ -97,7 +89,7 @@ def outbound(ks: KeySet, pt, iv, destination_hash, context, ifac, ifac_key, flag
     return framed, frame_off
 
 
-def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stream=None, aligned=False):
+def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stream=None, aligned=True):
     """One read of an interface's byte stream ``buf`` (uint8 on the device)
     through deframing, IFAC unmask (skipped for ``ifac_size`` 0, an interface
     without access codes: then frames with the IFAC flag set are dropped, as
@@ -118,23 +110,25 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
     outcome: ``status`` (RT_* token status; TOO_SHORT where there is no
     packet) with the plaintext at ``pt[pt_off[i]: pt_off[i] + pt_len[i]]``.
     Compacting first keeps the per-packet kernels' waves full (the gaps
-    between frames would otherwise be half of every wave).  With IFAC and
-    ``aligned`` the unmasked packets are written into 128-B-aligned slots (a
-    HEADER_1 packet's token ciphertext on a line, 128 B more buffer per pair)
-    and each plaintext starts on a line too; the default keeps them at their
-    stream offsets, which measured faster end to end (the decrypt gains 5 %,
-    the unmask writing into the slots loses more: DESIGN.md §4.8).  Only the
-    offsets differ."""
+    between frames would otherwise be half of every wave).  With ``aligned``
+    (default) the deframer writes every frame into its own 128-B-aligned slot
+    (rt_hdlc_deframe_slots: a HEADER_1 packet's token ciphertext on a line,
+    128 B more buffer per pair), the unmasked packets stay at those offsets
+    and each plaintext starts on a line too; otherwise frames sit at their
+    stream offsets.  Only the offsets differ (−8 % for the
+    path, mostly the unmask reading slotted frames)."""
     with _on(stream):      # temporaries allocated on the stream that uses them
         dev = buf.device
         # (at least one byte: an empty read still gives every later stage a
         # buffer to point at; no frame ever reaches into it)
-        out = torch.empty(max(buf.numel(), 1), dtype=torch.uint8, device=dev)
+        nout = device.deframe_slots_bytes(buf.numel(), max_pairs) if aligned else buf.numel()
+        out = torch.empty(max(nout, 1), dtype=torch.uint8, device=dev)
         d_off = torch.empty(max_pairs, dtype=torch.int64, device=dev)
         d_len = torch.empty(max_pairs, dtype=torch.int32, device=dev)
         d_st = torch.full((max_pairs,), -1, dtype=torch.int32, device=dev)
         counts = torch.empty(2, dtype=torch.int64, device=dev)
-        device.hdlc_deframe(buf, out, d_off, d_len, d_st, counts, hw_mtu=hw_mtu, ifac_size=ifac_size, stream=stream)
+        device.hdlc_deframe(buf, out, d_off, d_len, d_st, counts, hw_mtu=hw_mtu, ifac_size=ifac_size, stream=stream,
+                            line_phase=CT_PHASE if aligned else None)
         # the frames handed on, to the front in stream order; empty entries past them
         f_off = torch.empty(max_pairs, dtype=torch.int64, device=dev)
         f_len = torch.empty(max_pairs, dtype=torch.int32, device=dev)
@@ -142,25 +136,16 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
         n_frames = torch.empty((), dtype=torch.int64, device=dev)
         device.frames_compact(d_off, d_len, d_st, counts, f_off, f_len, frame_pair, n_frames, stream=stream)
         ifac = torch.empty((max_pairs, ifac_size), dtype=torch.uint8, device=dev)
-        pt_shift = 0
+        # with slots every frame (and the unmasked packet written at its
+        # offset) has its token ciphertext on a line, and each plaintext,
+        # written 16 B into its token's span, starts on one too
+        pt_shift = 16 if aligned else 0
         if ifac_size:
             ifac_status = torch.empty(max_pairs, dtype=torch.int32, device=dev)
             p_len = torch.empty(max_pairs, dtype=torch.int32, device=dev)
-            if aligned:
-                # slot i at the first offset >= f_off[i] + 128 i with the
-                # ciphertext phase; slots never overlap since frames do not
-                # (f_off[i+1] >= f_off[i] + f_len[i]) and each slot moves < 128 B
-                un = torch.empty(out.numel() + LINE * (max_pairs + 1), dtype=torch.uint8, device=dev)
-                base = _slot_base((un.data_ptr() + CT_PHASE) % LINE)
-                u_off = f_off + torch.arange(max_pairs, dtype=torch.int64, device=dev) * LINE
-                u_off += (base - u_off) % LINE
-                pt_shift = 16                 # plaintext i at its token + 16: on a line as well
-            else:
-                u_off = f_off
-                un = torch.empty_like(out)
-            device.ifac_unmask(out, f_off, f_len, ifac_key, ifac, un, u_off, ifac_status, out_len=p_len,
+            un = torch.empty_like(out)
+            device.ifac_unmask(out, f_off, f_len, ifac_key, ifac, un, f_off, ifac_status, out_len=p_len,
                                stream=stream)
-            f_off = u_off
         else:
             # no IFAC on the interface: a packet with the IFAC flag set is
             # dropped, the others go to unpack as they are

@@ -65,3 +65,15 @@ def test_c3_rate_small():
     r = bench.c3_rate(torch.device("cuda", 0), 8, n=8192, n_keys=97, steps=3)
     assert r["ok"] is True and r["packets"] == 8192
     assert r["encrypt"]["ms"] > 0 and r["decrypt"]["ms"] > 0 and r["round_trips_s"] > 0
+
+
+def test_node_host_rate_small():
+    """bench.node_host_rate (the composed interface path host-origin, in the
+    bench line) at a small size: both directions timed through pinned host
+    buffers, every slice's stream, every status and a sample of plaintexts
+    checked on the host copies."""
+    import torch
+    import bench
+    r = bench.node_host_rate(torch.device("cuda", 0), n=8192, slices=4, reps=1)
+    assert r["ok"] is True and r["packets"] == 8192
+    assert r["outbound"]["ms"] > 0 and r["inbound"]["ms"] > 0

@@ -142,8 +142,9 @@ def _check(res, stream, key, ifac_key, isz, hw_mtu):
     return seen, invalid
 
 
+@pytest.mark.parametrize("aligned", [False, True])
 @pytest.mark.parametrize("isz", [32, 16, 0])
-def test_inbound_edge_cases_match_the_oracle_composition(isz):
+def test_inbound_edge_cases_match_the_oracle_composition(isz, aligned):
     import torch
     import reticulum_amd as rt
     from reticulum_amd import pipeline
@@ -173,7 +174,7 @@ def test_inbound_edge_cases_match_the_oracle_composition(isz):
         masked.append(m if isz else bytes([raw[0] | 0x80]) + raw[1:])     # no IFAC: flagged copies must be dropped
     stream = _edge_stream(rng, good, masked, sent, max(isz, 1), hw_mtu, isz > 0)
     buf = torch.frombuffer(bytearray(stream), dtype=torch.uint8).to(dev)
-    res = pipeline.inbound(ks, buf, ik, isz, len(stream) // 2 + 2, hw_mtu=hw_mtu)
+    res = pipeline.inbound(ks, buf, ik, isz, len(stream) // 2 + 2, hw_mtu=hw_mtu, aligned=aligned)
     seen, invalid = _check(res, stream, key, ifac_key, isz, hw_mtu)
     # every case was exercised
     assert invalid and seen["ifac_drop"] and seen["ok"] >= n and seen["tok_fail"], seen
@@ -184,7 +185,8 @@ def test_inbound_edge_cases_match_the_oracle_composition(isz):
     assert sorted(ln[st == 1].tolist()) == sorted(invalid)
 
 
-def test_inbound_reads_split_across_calls_keep_the_loops_buffer():
+@pytest.mark.parametrize("aligned", [False, True])
+def test_inbound_reads_split_across_calls_keep_the_loops_buffer(aligned):
     """Two reads: the bytes the first leaves (counts[1] onwards, a partial
     frame) are carried into the second, as the read loop keeps them in its
     buffer; the frames of both reads together are the oracle's."""
@@ -209,7 +211,7 @@ def test_inbound_reads_split_across_calls_keep_the_loops_buffer():
     for chunk in (stream[:cut], stream[cut:]):
         data = carry + chunk
         res = pipeline.inbound(ks, torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev), ik, isz,
-                               len(data) // 2 + 2)
+                               len(data) // 2 + 2, aligned=aligned)
         torch.cuda.synchronize()
         nf = int(res["n_frames"])
         po, pl = res["pt_off"][:nf].cpu().numpy(), res["pt_len"][:nf].cpu().numpy()
@@ -220,8 +222,9 @@ def test_inbound_reads_split_across_calls_keep_the_loops_buffer():
     assert got == [pt[i].tobytes() for i in range(n)]
 
 
+@pytest.mark.parametrize("aligned", [False, True])
 @pytest.mark.parametrize("isz", [0, 16])
-def test_inbound_empty_read(isz):
+def test_inbound_empty_read(isz, aligned):
     """A zero-byte read (the read loop's empty recv) through the whole inbound
     path: no frames, nothing consumed, every entry empty (the
     no-IFAC branch gathered each entry's flag byte from an empty buffer)."""
@@ -231,10 +234,53 @@ def test_inbound_empty_read(isz):
     dev = torch.device("cuda", 0)
     ks = rt.KeySet(bytes(range(64)), device=0)
     ik = torch.arange(64, dtype=torch.uint8, device=dev)
-    res = pipeline.inbound(ks, torch.empty(0, dtype=torch.uint8, device=dev), ik, isz, 4)
+    res = pipeline.inbound(ks, torch.empty(0, dtype=torch.uint8, device=dev), ik, isz, 4, aligned=aligned)
     torch.cuda.synchronize()
     assert int(res["n_frames"]) == 0
     assert res["counts"].cpu().tolist() == [0, 0]
     assert (res["ifac_status"].cpu() == 1).all()
     assert (res["status"].cpu() == 1).all()
     assert (res["pt_len"].cpu() == 0).all()
+
+
+@pytest.mark.parametrize("phase", [0, 35, 127])
+def test_deframe_slots_match_stream_offsets(phase):
+    """rt_hdlc_deframe_slots against rt_hdlc_deframe on the edge-case stream
+    (junk, empty and oversized frames, escapes): the same pairs, lengths,
+    statuses, consumed bytes and frame bytes; each frame's byte `phase` on a
+    128-B line; frames disjoint inside the documented capacity."""
+    import torch
+    from reticulum_amd import device
+    rng = np.random.Generator(np.random.PCG64(77 + phase))
+    ow_frames = [ow.hdlc_frame(rng.integers(0, 256, int(rng.integers(1, 700)), dtype=np.uint8).tobytes())
+                 for _ in range(300)]
+    parts = []
+    for f in ow_frames:
+        r = rng.random()
+        parts.append(f if r > 0.1 else (b"\x7e\x7e" + f if r > 0.05 else f[:-1]))
+    stream = bytes(rng.integers(0, 256, 50, dtype=np.uint8)) + b"".join(parts) + b"\x7d\x5e\x7e\x7d"
+    dev = torch.device("cuda", 0)
+    buf = torch.frombuffer(bytearray(stream), dtype=torch.uint8).to(dev)
+    mp = len(stream) // 2 + 2
+    res = []
+    for ph in (None, phase):
+        out = torch.zeros(device.deframe_slots_bytes(buf.numel(), mp) if ph is not None else buf.numel(),
+                          dtype=torch.uint8, device=dev)
+        fo = torch.empty(mp, dtype=torch.int64, device=dev)
+        fl = torch.empty(mp, dtype=torch.int32, device=dev)
+        st = torch.full((mp,), -1, dtype=torch.int32, device=dev)
+        ct = torch.empty(2, dtype=torch.int64, device=dev)
+        device.hdlc_deframe(buf, out, fo, fl, st, ct, hw_mtu=500, ifac_size=0, line_phase=ph)
+        torch.cuda.synchronize()
+        res.append((out, fo.cpu().numpy(), fl.cpu().numpy(), st.cpu().numpy(), ct.cpu().tolist()))
+    (o0, f0, l0, s0, c0), (o1, f1, l1, s1, c1) = res
+    pairs = c0[0]
+    assert c0 == c1 and pairs > 300
+    assert (l0[:pairs] == l1[:pairs]).all() and (s0[:pairs] == s1[:pairs]).all()
+    b0, b1 = o0.cpu().numpy(), o1.cpu().numpy()
+    ends = []
+    for k in range(pairs):
+        assert b0[f0[k]:f0[k] + l0[k]].tobytes() == b1[f1[k]:f1[k] + l1[k]].tobytes(), k
+        assert (o1.data_ptr() + int(f1[k]) + phase) % 128 == 0, k
+        ends.append((int(f1[k]), int(f1[k]) + int(l1[k])))
+    assert all(a[1] <= b[0] for a, b in zip(ends, ends[1:])) and ends[-1][1] <= o1.numel()

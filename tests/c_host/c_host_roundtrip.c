@@ -140,7 +140,7 @@ static void token_batch(rt_ctx *c, rt_keyset *ks, const uint8_t *keys) {
 
 enum { NP = 3001, PL = 383, ISZ = 16, HDR = 19 };
 
-static void interface_path(rt_ctx *c, rt_keyset *ks, const uint8_t *key) {
+static void interface_path(rt_ctx *c, rt_keyset *ks, const uint8_t *key, int slots) {
     const uint32_t tl = (uint32_t)rt_token_len(PL), rl = HDR + tl, ml = rl + ISZ;
     uint8_t *pt = malloc((uint64_t)NP * PL), *iv = malloc(16 * NP), *dh = malloc(16 * NP), *ctx = malloc(NP);
     uint8_t *ifac = malloc((uint64_t)NP * ISZ), ikey[64];
@@ -170,9 +170,11 @@ static void interface_path(rt_ctx *c, rt_keyset *ks, const uint8_t *key) {
     d2h(c, &total, d_foff + NP, 8);              /* the stream's length: what a socket write needs */
     CHECK(total > (uint64_t)NP * (ml + 2) && total <= fcap, "framed length %llu", (unsigned long long)total);
 
-    /* inbound: one read of that stream, no host sync until the plaintexts */
-    const uint64_t mp = 2 * NP;
-    uint8_t *d_out = dalloc(c, total), *d_un = dalloc(c, total), *d_ptb = dalloc(c, total);
+    /* inbound: one read of that stream, no host sync until the plaintexts;
+     * with slots, every frame in its own 128-B-aligned slot (token ciphertext
+     * of the unmasked packet on a line) */
+    const uint64_t mp = 2 * NP, cap = slots ? total + 128 * (mp + 1) : total;
+    uint8_t *d_out = dalloc(c, cap), *d_un = dalloc(c, cap), *d_ptb = dalloc(c, cap);
     uint8_t *d_ifo = dalloc(c, mp * ISZ);
     uint64_t *d_doff = dalloc(c, 8 * mp), *d_counts = dalloc(c, 16), *d_coff = dalloc(c, 8 * mp);
     uint64_t *d_toff = dalloc(c, 8 * mp);
@@ -183,7 +185,11 @@ static void interface_path(rt_ctx *c, rt_keyset *ks, const uint8_t *key) {
     rt_packet_fields *d_fields = dalloc(c, sizeof(rt_packet_fields) * mp);
     void *d_dws = dalloc(c, rt_hdlc_deframe_workspace_bytes(total));
     void *d_cws = dalloc(c, rt_frames_compact_workspace_bytes(mp));
-    RT(rt_hdlc_deframe(c, d_framed, total, 262144, ISZ, d_out, d_doff, d_dlen, d_dst, d_counts, mp, d_dws, NULL));
+    if (slots)
+        RT(rt_hdlc_deframe_slots(c, d_framed, total, 262144, ISZ, HDR + 16, d_out, d_doff, d_dlen, d_dst, d_counts, mp,
+                                 d_dws, NULL));
+    else
+        RT(rt_hdlc_deframe(c, d_framed, total, 262144, ISZ, d_out, d_doff, d_dlen, d_dst, d_counts, mp, d_dws, NULL));
     RT(rt_frames_compact(c, d_doff, d_dlen, d_dst, d_counts, mp, d_coff, d_clen, d_pair, d_nf, d_cws, NULL));
     RT(rt_ifac_unmask(c, d_out, d_coff, d_clen, ISZ, d_ikey, 64, d_ifo, d_un, d_coff, d_ist, d_plen, (uint32_t)mp,
                       NULL));
@@ -197,9 +203,9 @@ static void interface_path(rt_ctx *c, rt_keyset *ks, const uint8_t *key) {
     int32_t *st = malloc(4 * mp), *ist = malloc(4 * mp);
     uint32_t *olen = malloc(4 * mp);
     uint64_t *toff = malloc(8 * mp);
-    uint8_t *ifo = malloc(mp * ISZ), *back = malloc(total), *un = malloc(total), *ref = malloc(tl);
+    uint8_t *ifo = malloc(mp * ISZ), *back = malloc(cap), *un = malloc(cap), *ref = malloc(tl);
     d2h(c, st, d_st, 4 * mp); d2h(c, ist, d_ist, 4 * mp); d2h(c, olen, d_olen, 4 * mp);
-    d2h(c, toff, d_toff, 8 * mp); d2h(c, ifo, d_ifo, mp * ISZ); d2h(c, back, d_ptb, total); d2h(c, un, d_un, total);
+    d2h(c, toff, d_toff, 8 * mp); d2h(c, ifo, d_ifo, mp * ISZ); d2h(c, back, d_ptb, cap); d2h(c, un, d_un, cap);
     CHECK(memcmp(ifo, ifac, (uint64_t)NP * ISZ) == 0, "IFACs");
     for (int i = 0; i < NP; ++i) {
         CHECK(ist[i] == 0 && st[i] == RT_ST_OK && olen[i] == PL, "packet %d: ifac %d token %d len %u", i, ist[i],
@@ -207,6 +213,7 @@ static void interface_path(rt_ctx *c, rt_keyset *ks, const uint8_t *key) {
         CHECK(memcmp(back + toff[i], pt + (uint64_t)i * PL, PL) == 0, "plaintext %d", i);
         oracle_token_encrypt(key, 64, iv + 16 * i, pt + (uint64_t)i * PL, PL, ref);
         CHECK(memcmp(un + toff[i], ref, tl) == 0, "token %d differs from the oracle's", i);
+        CHECK(!slots || ((uintptr_t)d_un + toff[i] + 16) % 128 == 0, "slot %d: ciphertext not on a line", i);
     }
     for (uint64_t i = NP; i < mp; ++i) CHECK(st[i] == RT_ST_TOO_SHORT, "entry %llu past the frames: status %d",
                                            (unsigned long long)i, st[i]);
@@ -286,7 +293,8 @@ int main(void) {
     token_batch(c, ks, keys);
     rt_keyset *k1 = rt_keyset_create(c, keys, 64, 1);
     CHECK(k1 != NULL, "rt_keyset_create");
-    interface_path(c, k1, keys);
+    interface_path(c, k1, keys, 0);
+    interface_path(c, k1, keys, 1);
     clock_and_copies(c, k1);
     rt_keyset_destroy(k1);
     rt_keyset_destroy(ks);

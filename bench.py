@@ -420,6 +420,9 @@ def main():
             node["host"] = {"error": f"{type(exc).__name__}: {exc}"}
         try:
             c5share = c5_share_rate(dev, _native.load().rt_num_cus(_native.context(local)))
+            # the same packets, each in its own 128-B-aligned slot
+            al = c5_share_rate(dev, _native.load().rt_num_cus(_native.context(local)), align=True)
+            c5share["aligned_slots"] = {k: al[k] for k in ("ok", "layout", "encrypt", "decrypt")}
         except Exception as exc:
             c5share = {"error": f"{type(exc).__name__}: {exc}"}
         try:
@@ -1365,7 +1368,7 @@ def per_call_rate(threads=16, calls=200, L=383, seconds_cap=20.0):
     return res
 
 
-def c5_share_rate(dev, n_cu, n=1 << 20, steps=10, n_keys=65536):
+def c5_share_rate(dev, n_cu, n=1 << 20, steps=10, n_keys=65536, align=False):
     """The per-rank shape of c5 at 8 GPUs (8 M packets of
     64-4096 B, 65 536 keys, 50/50 encrypt/decrypt; one rank's share is 2^20
     packets), device-resident on this GPU through the product's packed entry
@@ -1376,7 +1379,9 @@ def c5_share_rate(dev, n_cu, n=1 << 20, steps=10, n_keys=65536):
     per direction after the clock warmup; canonical ops summed over the real
     lengths (352 per AES block, 1464 per SHA-256 compression,
     +8 per tag compare); every decrypt status and length checked, and a
-    sample of plaintexts and tokens against each other (round trip)."""
+    sample of plaintexts and tokens against each other (round trip).
+    ``align``: every packet in its own 128-B-aligned slot (plaintexts on a
+    line, each token's ciphertext on a line) instead of end to end."""
     import torch
     import reticulum_amd as rt
     from reticulum_amd import device
@@ -1389,27 +1394,33 @@ def c5_share_rate(dev, n_cu, n=1 << 20, steps=10, n_keys=65536):
     h = n // 2
     le, ld = lens[:h].to(dev), lens[h:].to(dev)
 
-    def offs(x):
+    def offs(x, phase=0):
+        w = x.to(torch.int64)
+        if align:
+            w = (w + 127) // 128 * 128
         o = torch.zeros(x.numel(), dtype=torch.int64, device=dev)
-        o[1:] = torch.cumsum(x[:-1].to(torch.int64), 0)
-        return o
+        o[1:] = torch.cumsum(w[:-1], 0)
+        return o + ((-phase) % 128 if align else 0)
+
+    def span(o, x):
+        return int(o[-1]) + int(x[-1]) + 1
 
     tlen = lambda x: (16 + 16 * (x // 16 + 1) + 32).to(torch.int32)     # noqa: E731
     # encrypt half: plaintexts -> tokens
-    pe = torch.randint(0, 256, (int(le.to(torch.int64).sum()),), dtype=torch.uint8, device=dev, generator=g)
     oe, ive = offs(le), torch.randint(0, 256, (h, 16), dtype=torch.uint8, device=dev, generator=g)
+    pe = torch.randint(0, 256, (span(oe, le),), dtype=torch.uint8, device=dev, generator=g)
     te_len = tlen(le)
-    te_off = offs(te_len)
-    te = torch.empty(int(te_len.to(torch.int64).sum()), dtype=torch.uint8, device=dev)
+    te_off = offs(te_len, 16)
+    te = torch.empty(span(te_off, te_len), dtype=torch.uint8, device=dev)
     # decrypt half: tokens made before timing
-    pd = torch.randint(0, 256, (int(ld.to(torch.int64).sum()),), dtype=torch.uint8, device=dev, generator=g)
     od, ivd = offs(ld), torch.randint(0, 256, (n - h, 16), dtype=torch.uint8, device=dev, generator=g)
+    pd = torch.randint(0, 256, (span(od, ld),), dtype=torch.uint8, device=dev, generator=g)
     td_len = tlen(ld)
-    td_off = offs(td_len)
-    td = torch.empty(int(td_len.to(torch.int64).sum()), dtype=torch.uint8, device=dev)
+    td_off = offs(td_len, 16)
+    td = torch.empty(span(td_off, td_len), dtype=torch.uint8, device=dev)
     device.encrypt(ks, pd, od, ld, ivd, td, td_off, key_idx=kidx[h:], sort=True)
-    back = torch.empty(int((td_len - 48).to(torch.int64).sum()), dtype=torch.uint8, device=dev)
     boff = offs(td_len - 48)
+    back = torch.empty(span(boff, td_len - 48), dtype=torch.uint8, device=dev)
     ol = torch.empty(n - h, dtype=torch.int32, device=dev)
     st = torch.empty(n - h, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -1421,13 +1432,14 @@ def c5_share_rate(dev, n_cu, n=1 << 20, steps=10, n_keys=65536):
     torch.cuda.synchronize()
     ok = bool((st == 0).all()) and torch.equal(ol, ld)
     # round trip of a sample of the encrypt half's tokens, and the decrypt half's plaintexts
-    chk = torch.empty(int((te_len - 48).to(torch.int64).sum()), dtype=torch.uint8, device=dev)
+    coff = offs(te_len - 48)
+    chk = torch.empty(span(coff, te_len - 48), dtype=torch.uint8, device=dev)
     cl = torch.empty(h, dtype=torch.int32, device=dev)
     cs = torch.empty(h, dtype=torch.int32, device=dev)
-    device.decrypt(ks, te, te_off, te_len, chk, offs(te_len - 48), cl, cs, key_idx=kidx[:h], sort=True)
+    device.decrypt(ks, te, te_off, te_len, chk, coff, cl, cs, key_idx=kidx[:h], sort=True)
     torch.cuda.synchronize()
     ok = ok and bool((cs == 0).all()) and torch.equal(cl, le)
-    co = offs(te_len - 48).cpu()
+    co = coff.cpu()
     oe_c, od_c, bo_c = oe.cpu(), od.cpu(), boff.cpu()
     for i in range(0, h, 4099):
         a, b, L = int(co[i]), int(oe_c[i]), int(lens[i])
@@ -1442,7 +1454,8 @@ def c5_share_rate(dev, n_cu, n=1 << 20, steps=10, n_keys=65536):
     peak = n_cu * 128 * 2.4e9
     res = {"packets": n, "keys": n_keys, "encrypt_packets": h, "decrypt_packets": n - h,
            "plaintext_bytes": int(L64.sum()), "mean_plaintext_bytes": float(L64.float().mean()), "ok": ok,
-           "layout": "packed rows (byte strings at prefix-sum offsets), length-bucketed on the device"}
+           "layout": ("byte strings in 128-B-aligned slots (prefix sums of whole lines)" if align else
+                      "packed rows (byte strings at prefix-sum offsets)") + ", length-bucketed on the device"}
     for name, f, o, bytes_ in (("encrypt", enc, ops_e, int(L64[:h].sum())), ("decrypt", dec, ops_d, int(L64[h:].sum()))):
         warmup(f, stream, 2, 0.3)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]

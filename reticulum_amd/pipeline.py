@@ -89,7 +89,7 @@ def outbound(ks: KeySet, pt, iv, destination_hash, context, ifac, ifac_key, flag
     return framed, frame_off
 
 
-def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stream=None, aligned=True):
+def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stream=None, aligned=None):
     """One read of an interface's byte stream ``buf`` (uint8 on the device)
     through deframing, IFAC unmask (skipped for ``ifac_size`` 0, an interface
     without access codes: then frames with the IFAC flag set are dropped, as
@@ -111,12 +111,17 @@ def inbound(ks: KeySet, buf, ifac_key, ifac_size, max_pairs, hw_mtu=262144, stre
     packet) with the plaintext at ``pt[pt_off[i]: pt_off[i] + pt_len[i]]``.
     Compacting first keeps the per-packet kernels' waves full (the gaps
     between frames would otherwise be half of every wave).  With ``aligned``
-    (default) the deframer writes every frame into its own 128-B-aligned slot
+    the deframer writes every frame into its own 128-B-aligned slot
     (rt_hdlc_deframe_slots: a HEADER_1 packet's token ciphertext on a line,
-    128 B more buffer per pair), the unmasked packets stay at those offsets
-    and each plaintext starts on a line too; otherwise frames sit at their
-    stream offsets.  Only the offsets differ (−8 % for the
-    path, mostly the unmask reading slotted frames)."""
+    128 B more buffer per pair of max_pairs), the unmasked packets stay at
+    those offsets and each plaintext starts on a line too; otherwise frames
+    sit at their stream offsets.  Only the offsets differ (DESIGN.md §4.8:
+    −8 % for the path, mostly the unmask reading slotted frames).  The default
+    (None) takes slots when their padding is at most the stream's own size
+    (a Reticulum stream has about two pairs per packet; a max_pairs sized for
+    a stream of nothing but flags would multiply the buffers instead)."""
+    if aligned is None:
+        aligned = device.LINE * (max_pairs + 1) <= buf.numel()
     with _on(stream):      # temporaries allocated on the stream that uses them
         dev = buf.device
         # (at least one byte: an empty read still gives every later stage a

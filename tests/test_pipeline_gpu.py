@@ -150,3 +150,30 @@ def test_aligned_slots_change_only_offsets(n, L, isz):
     pa, pp = ra["pt"].cpu().numpy(), rp["pt"].cpu().numpy()
     for i in range(n):
         assert pa[poa[i]:poa[i] + L].tobytes() == pp[pop[i]:pop[i] + L].tobytes() == pt[i].tobytes(), i
+
+
+def test_inbound_slots_by_default_when_padding_fits():
+    """pipeline.inbound's default: slots when their padding (128 B per flag
+    pair allowed) is at most the stream's size, stream offsets otherwise (a
+    max_pairs sized for a stream of nothing but flags); same results both ways."""
+    import torch
+    import reticulum_amd as rt
+    from reticulum_amd import pipeline
+    n, L, isz = 1000, 383, 16
+    key, ifac_key, pt, iv, dh, ctx, ifac, t = _case(n, L, isz, 4321)
+    ks = rt.KeySet(key, device=0)
+    ik = t(np.frombuffer(ifac_key, np.uint8))
+    framed, foff = pipeline.outbound(ks, t(pt), t(iv), t(dh), t(ctx), t(ifac), ik)
+    buf = framed[:int(foff[-1])].clone()
+    auto = pipeline.inbound(ks, buf, ik, isz, 2 * n)
+    wide = pipeline.inbound(ks, buf, ik, isz, buf.numel() // 2 + 2)
+    packed = pipeline.inbound(ks, buf, ik, isz, 2 * n, aligned=False)
+    torch.cuda.synchronize()
+    po = auto["pt_off"][:n].cpu().numpy()
+    assert ((auto["pt"].data_ptr() + po) % 128 == 0).all()                  # slots
+    assert torch.equal(wide["pt_off"][:n], packed["pt_off"][:n])             # stream offsets
+    assert auto["pt"].numel() > packed["pt"].numel() == wide["pt"].numel()
+    for r in (auto, wide):
+        assert torch.equal(r["status"][:n], packed["status"][:n]) and torch.equal(r["ifac"][:n], packed["ifac"][:n])
+        p, o = r["pt"].cpu().numpy(), r["pt_off"][:n].cpu().numpy()
+        assert all(p[o[i]:o[i] + L].tobytes() == pt[i].tobytes() for i in range(0, n, 7))

@@ -356,20 +356,29 @@ def main():
             raise SystemExit("bench: round trip failed on the aligned-slot batch")
 
     def timed(step):
+        """The timed steps run unstamped (stamping adds a
+        workgroup barrier and four atomics per workgroup to every launch);
+        the in-run clock comes from a stamped pass of the same steps right
+        after them, whose elapsed time is reported beside the headline's."""
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-        clock = device.LaunchClock(dev)      # the timed launches stamp their own clock (rt_clock_stamps)
+        clock = device.LaunchClock(dev)      # the stamped pass (rt_clock_stamps)
         if world > 1:
             dist.barrier()
         warm = warmup(step, stream, args.warmup, args.warmup_seconds)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(evs[k])
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
         with clock:
-            t0 = time.perf_counter()
+            t2 = time.perf_counter()
             for k in range(args.steps):
-                step(evs[k])
+                step()
             torch.cuda.synchronize()
-            t1 = time.perf_counter()
+            t3 = time.perf_counter()
         if world > 1:
             dist.barrier()
         el = t1 - t0
@@ -380,7 +389,12 @@ def main():
             t = torch.tensor([el, e_avg, d_avg], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el, e_avg, d_avg = t.tolist()
-        return el, e_avg, d_avg, e_ms, d_ms, warm, clock.summary()
+        clk = clock.summary()
+        clk["stamped_pass_ms_per_step"] = (t3 - t2) / args.steps * 1e3
+        clk["unstamped_ms_per_step"] = (t1 - t0) / args.steps * 1e3
+        clk["note"] = ("from a stamped pass of the same steps right after the timed (unstamped) ones; "
+                       "stamped_pass_ms_per_step vs unstamped_ms_per_step is the stamps' cost on this box")
+        return el, e_avg, d_avg, e_ms, d_ms, warm, clk
 
     elapsed, enc_avg, dec_avg, enc_ms, dec_ms, (warm_steps, warm_s), clk = timed(steps[layouts[0]])
     other = None
@@ -508,7 +522,7 @@ def main():
                      "ops_per_packet": ops_dec(L) if dom == "decrypt" else ops_enc(L),
                      "algorithmic_bytes_per_launch": hbm_bytes,
                      "algorithmic_hbm_gb_s": hbm_bytes / (dom_ms * 1e-3) / 1e9,
-                     "frac_of_survey_P": achieved / (n_cu * 64 * 2.4e9),
+                     **ceiling_fracs(dom, L, args.keys, achieved / peak_valu),
                      "in_run_clock": in_run,
                      "cycles_per_launch": (in_run.get(dom) or {}).get("cycles_per_launch"),
                      "clock_ghz": (in_run.get(dom) or {}).get("clock_ghz"),
@@ -527,7 +541,11 @@ def main():
                              "clock_ghz / cycles_per_launch / frac_at_measured_clock are measured in THIS run: every "
                              "workgroup of the timed launches stamps its span in shader cycles and 100 MHz ticks "
                              "(rt_clock_stamps; in_run_clock has both kernels); sustained_clock_ghz_committed_pmc is "
-                             "the builder's PMC run (GRBM_GUI_ACTIVE / 8 XCDs / kernel-trace average); frac_of_survey_P uses BASELINE.md §5's P = CUs x 64 x 2.4 GHz; traffic = HBM "
+                             "the builder's PMC run (GRBM_GUI_ACTIVE / 8 XCDs / kernel-trace average); ceiling_frac = the "
+                             "guide-peak fraction this instruction stream reaches at most (its ISA slot floor: every "
+                             "dual-issuable op paired, every LDS lookup a slot), ceiling_frac_valu_only the same with "
+                             "every lookup hidden behind other waves' VALU issue; frac_over_ceiling = frac / "
+                             "ceiling_frac (DESIGN.md §4.5); traffic = HBM "
                              "bytes per launch from the committed rocprofv3 PMC summary (profiles/*_pmc.json, FETCH_SIZE "
                              "x 2 + WRITE_SIZE; see traffic_detail.calibration). issue_model = the kernel's issue slots "
                              "from its ISA (floor: every dual-issuable op paired; ceiling: none), its issued slots from "
@@ -976,6 +994,28 @@ SLOTS_PER_WAVE_PACKET_500B = {
     "encrypt": {"floor": 1929 + 7 * 3030 + 3 * 1102, "ceiling": 2290 + 7 * 3666 + 3 * 1385},
     "decrypt": {"floor": 8 * 3039 + 2 * 1095, "ceiling": 8 * 3724 + 2 * 1375},
 }
+# LDS lookups (ds_read_b32) per wave-packet inside those slot counts: 896 per
+# AES quad (16 per block-round, 14 rounds, 4 blocks)
+LOOKUP_SLOTS_PER_WAVE_PACKET_500B = {"encrypt": 8 * 896, "decrypt": 8 * 896}
+
+
+def ceiling_fracs(kernel, L, keys, frac):
+    """The guide-peak fraction the running instruction stream can reach at
+    most (c2 shape: 500 B, one key), from its ISA slot floor: the peak is two
+    wave64 VALU instructions per SIMD slot, so canonical lane-ops / (slots x
+    128).  ceiling_frac charges every LDS lookup a slot (the issue-slot model
+    of DESIGN.md §4.5); ceiling_frac_valu_only lets other waves' VALU work
+    hide every lookup (tools/coissue_probe.hip).  None off the c2 shape."""
+    if L != 500 or keys != 1 or kernel not in SLOTS_PER_WAVE_PACKET_500B:
+        return {"ceiling_frac": None, "ceiling_frac_valu_only": None, "frac_over_ceiling": None}
+    ops = 64 * (ops_dec(L) if kernel == "decrypt" else ops_enc(L))
+    floor = SLOTS_PER_WAVE_PACKET_500B[kernel]["floor"]
+    c = ops / (floor * 128)
+    cv = ops / ((floor - LOOKUP_SLOTS_PER_WAVE_PACKET_500B[kernel]) * 128)
+    return {"ceiling_frac": c, "ceiling_frac_valu_only": cv, "frac_over_ceiling": frac / c,
+            "frac_over_ceiling_valu_only": frac / cv}
+
+
 # The same per-wave-packet composition measured instead of counted: the
 # kernels' own enc_quad / dec_quad / sha256_compress in register-only loops
 # at c2's launch shape (tools/floor_probe.hip, profiles/r02af_floor_probe.txt;
@@ -994,7 +1034,7 @@ def in_run_clock(summary, dom, achieved, n_cu, event_ms):
     the roofline fraction against the peak at that clock (CUs x 128 lanes x
     the measured clock instead of 2.4 GHz), which separates the code from the
     box's clock."""
-    out = {k: dict(v, event_ms=event_ms.get(k)) for k, v in summary.items()}
+    out = {k: (dict(v, event_ms=event_ms.get(k)) if isinstance(v, dict) else v) for k, v in summary.items()}
     d = out.get(dom)
     if d:
         out["frac_at_measured_clock"] = achieved / (n_cu * 128 * d["clock_ghz"] * 1e9)

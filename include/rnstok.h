@@ -72,7 +72,7 @@
 extern "C" {
 #endif
 
-#define RNSTOK_ABI_VERSION 1
+#define RNSTOK_ABI_VERSION 2   /* 2: rt_hdlc_deframe_slots, rt_clock_stamps */
 
 /* Return codes (< 0: API misuse or runtime failure). */
 #define RT_OK        0

@@ -17,6 +17,9 @@ RT_F_SORT_BY_LENGTH = 1
 RT_ST_OK, RT_ST_TOO_SHORT, RT_ST_BAD_HMAC, RT_ST_BAD_CT_LEN, RT_ST_BAD_PAD = 0, 1, 2, 3, 4
 RT_KERNEL_GENERAL, RT_KERNEL_ENC_LONG4, RT_KERNEL_ENC_LONG, RT_KERNEL_DEC_LONG2 = 0, 1, 2, 3
 RT_KERNEL_ENC_SPLIT = 4
+# the RNSTOK_ABI_VERSION (include/rnstok.h) these bindings are written for;
+# load() refuses any other build of the library
+ABI_VERSION = 2
 
 # (name, restype, argtypes) for every entry point declared in include/rnstok.h
 _vp, _u32, _u64, _i32, _int = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int
@@ -132,10 +135,17 @@ def load():
                 lib = ctypes.CDLL(LIB_PATH)
             except OSError as e:
                 raise NativeUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+            missing = [name for name, _, _ in SIGNATURES if not hasattr(lib, name)]
+            if missing:
+                raise NativeUnavailable(f"{LIB_PATH} is older than these bindings (missing {', '.join(missing[:4])}"
+                                        f"{' ...' if len(missing) > 4 else ''}): rebuild it")
             for name, res, args in SIGNATURES:
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
+            if lib.rt_abi_version() != ABI_VERSION:
+                raise NativeUnavailable(f"{LIB_PATH} has ABI version {lib.rt_abi_version()}, these bindings expect "
+                                        f"{ABI_VERSION}: rebuild it")
             _lib = lib
     return _lib
 
@@ -171,6 +181,18 @@ def context(device=None):
     return ctx
 
 
+def unavailable_reason(device=None):
+    """None when librnstok.so loads and a gfx950 device answers rt_create,
+    else why not (the message of the failure)."""
+    try:
+        context(device)
+        return None
+    except (NativeUnavailable, OSError, ValueError) as e:
+        # OSError: the runtime itself fails to load; ValueError: a bad
+        # RNSTOK_DEVICE value.  Either way the caller takes the reference path.
+        return str(e)
+
+
 def available(device=None):
     """True when librnstok.so loads and a gfx950 device answers rt_create.
 
@@ -178,8 +200,4 @@ def available(device=None):
     without the library or the GPU falls back to the reference's Token the
     way RNS/Cryptography/Provider.py:43-61 always leaves a working backend,
     instead of every Link.decrypt returning None (RNS/Link.py:1175-1182)."""
-    try:
-        context(device)
-        return True
-    except NativeUnavailable:
-        return False
+    return unavailable_reason(device) is None

@@ -38,6 +38,15 @@ namespace rnstok {
 #ifndef RNSTOK_DEC_PAIR              // decrypt, one key, token quads loaded in pairs: fetch -21 %, time -1.6 %
 #define RNSTOK_DEC_PAIR 1
 #endif
+#ifndef RNSTOK_DEC_TOUCH             // decrypt pairs: odd quads touch the next pair's first line in L2
+#define RNSTOK_DEC_TOUCH 0
+#endif
+#ifndef RNSTOK_DEC_TAG_LAST          // decrypt: tag units loaded at the start of the last quad
+#define RNSTOK_DEC_TAG_LAST 0
+#endif
+#ifndef RNSTOK_DEC_ST_SC1            // decrypt: plaintext stores with sc1 (experiment)
+#define RNSTOK_DEC_ST_SC1 0
+#endif
 #ifndef RNSTOK_SPLIT_DYN              // split encrypt: unevenly divided uniform batches from a counter
 #define RNSTOK_SPLIT_DYN 1
 #endif
@@ -1074,7 +1083,8 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
             u32x4 prev = ld16(Kt);
             // (RNSTOK_DEC_TAG_EARLY: the tag's two units loaded before the quad
             // loop, so the compare after it does not wait on them)
-            constexpr bool TAG_EARLY = RNSTOK_DEC_TAG_EARLY && !PERKEY && WG <= 768;
+            constexpr bool TAG_LAST = RNSTOK_DEC_TAG_LAST && !ILV && !PERKEY && WG <= 768;
+            constexpr bool TAG_EARLY = RNSTOK_DEC_TAG_EARLY && !TAG_LAST && !PERKEY && WG <= 768;
             u32x4 tag0, tag1;
             if (TAG_EARLY) {
                 tag0 = ld16(Kt + US * ((T >> 4) - 2u));
@@ -1090,12 +1100,26 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
             // L2 through and the line is fetched again: 2.7x read traffic)
             constexpr bool PAIR = RNSTOK_DEC_PAIR && !ILV && !PERKEY && WG <= 768;   // (1024: 11 -> 38 VGPRs spilled)
             u32x4 nx[4];
+            uint32_t touch = 0u;
 #pragma nounroll
             for (uint32_t q = 0; q <= nq; ++q) {
                 const uint32_t nbk = q < nq ? 4u : tb;
+                if (TAG_LAST && q == nq) {
+                    tag0 = ld16(Kt + US * ((T >> 4) - 2u));
+                    tag1 = ld16(Kt + US * ((T >> 4) - 1u));
+                }
                 if (PAIR && (q & 1u)) {
 #pragma unroll
                     for (int k = 0; k < 4; ++k) c[k] = nx[k];
+                    // the next pair's first unit usually shares a 128-B line
+                    // with this pair's last; an L2-served touch one quad
+                    // before it is needed keeps the line from being evicted
+                    if (RNSTOK_DEC_TOUCH == 1 && q < nq)
+                        (void)*(volatile const __attribute__((address_space(1))) uint32_t *)(uintptr_t)(C + 4 * US);
+                    if (RNSTOK_DEC_TOUCH == 2 && q < nq)
+                        touch = __hip_atomic_load((const uint32_t *)(C + 4 * US), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (RNSTOK_DEC_TOUCH == 3 && q < nq)
+                        asm volatile("global_load_dword %0, %1, off" : "=v"(touch) : "v"(C + 4 * US) : "memory");
                 } else {
                     c[0] = ld16(C);
                     c[1] = nbk > 1u ? ld16(C + US) : z;
@@ -1111,16 +1135,32 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
                 }
                 S.start(h);
                 sha_units(S.w, prev, c[0], c[1], c[2]);
+                // (the touch's register is released only after a later load's
+                // data was waited for: vmcnt counts in issue order)
+                if (RNSTOK_DEC_TOUCH >= 2 && PAIR && !(q & 1u)) asm volatile("" ::"v"(touch));
                 dec_quad<NR, true>(pp, c, prev, K.rk, LN, S);
 #pragma unroll
                 for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(S.v[k]));   // see k_encrypt
                 const bool keep = nbk >= 3u;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) h[k] += keep ? S.v[k] : 0u;
-                st16(D, pp[0]);
-                if (nbk > 1u) st16(D + US, pp[1]);
-                if (nbk > 2u) st16(D + 2 * US, pp[2]);
-                if (nbk > 3u) st16(D + 3 * US, pp[3]);
+#if RNSTOK_DEC_ST_SC1
+                // experiment: write-through stores that drop their line from L2
+                // (MI355X_MICROARCH.md: sc1 stores do not keep the line), so
+                // the L2 holds the token lines the next pair shares
+                if (!ILV && !PERKEY) {
+                    st16_sc1(D, pp[0]);
+                    if (nbk > 1u) st16_sc1(D + US, pp[1]);
+                    if (nbk > 2u) st16_sc1(D + 2 * US, pp[2]);
+                    if (nbk > 3u) st16_sc1(D + 3 * US, pp[3]);
+                } else
+#endif
+                {
+                    st16(D, pp[0]);
+                    if (nbk > 1u) st16(D + US, pp[1]);
+                    if (nbk > 2u) st16(D + 2 * US, pp[2]);
+                    if (nbk > 3u) st16(D + 3 * US, pp[3]);
+                }
                 prev = c[3];
                 C += 4 * US; D += 4 * US;
             }
@@ -1129,7 +1169,7 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
             // pp[0..tb-1] its plaintext
             const u32x4 pb = ld16(Kt + 4ull * US * nq);
             u32x4 r0, r1;
-            if (TAG_EARLY) {
+            if (TAG_EARLY || TAG_LAST) {
                 r0 = tag0;
                 r1 = tag1;
             } else {

@@ -5,6 +5,8 @@ buffer is a CUDA(HIP) tensor already resident in HBM, the kernels are
 enqueued on the given stream (default: torch's current stream) and nothing is
 synchronised.  torch is used only for device memory and streams.
 """
+import threading
+
 import torch
 
 from . import _native
@@ -596,22 +598,48 @@ class LaunchClock:
         with device.LaunchClock(dev) as lc:
             ...launches...
         lc.summary()      # syncs the device, then clock_summary(words)
-    """
+
+    Stamping is per context, i.e. process-wide for the device: every launch
+    on it from any thread or stream while the block is open is stamped into
+    this object's words.  One block per device at a time (a nested or
+    concurrent block raises RuntimeError instead of mixing stamps), and the
+    exit waits for the device, so no launch still adds to the words once the
+    block is closed."""
+
+    _open = set()               # device indices with an open block
+    _open_lock = threading.Lock()
 
     def __init__(self, dev=None):
         dev = torch.device("cuda", torch.cuda.current_device()) if dev is None else torch.device(dev)
         self.dev = dev
+        self._index = dev.index if dev.index is not None else torch.cuda.current_device()
         self.acc = torch.zeros(8, dtype=torch.int64, device=dev)
-        self._ctx = _native.context(dev.index if dev.index is not None else torch.cuda.current_device())
+        self._ctx = _native.context(self._index)
 
     def __enter__(self):
-        # the zeroed words are ordered before any launch the block enqueues
-        torch.cuda.synchronize(self.dev)
-        _native.check(_native.load().rt_clock_stamps(self._ctx, self.acc.data_ptr()))
+        with LaunchClock._open_lock:
+            if self._index in LaunchClock._open:
+                raise RuntimeError(f"a LaunchClock is already open on cuda:{self._index}: stamping is per context")
+            LaunchClock._open.add(self._index)
+        try:
+            # the zeroed words are ordered before any launch the block enqueues
+            torch.cuda.synchronize(self.dev)
+            _native.check(_native.load().rt_clock_stamps(self._ctx, self.acc.data_ptr()))
+        except BaseException:
+            with LaunchClock._open_lock:
+                LaunchClock._open.discard(self._index)
+            raise
         return self
 
     def __exit__(self, *exc):
-        _native.check(_native.load().rt_clock_stamps(self._ctx, None))
+        try:
+            _native.check(_native.load().rt_clock_stamps(self._ctx, None))
+            # launches already queued still add to acc: let them land before
+            # the block counts as closed (and before acc can be freed)
+            torch.cuda.synchronize(self.dev)
+        finally:
+            with LaunchClock._open_lock:
+                LaunchClock._open.discard(self._index)
         return False
 
     def words(self):

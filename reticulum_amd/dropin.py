@@ -14,11 +14,12 @@ does (RNS/Cryptography/Provider.py:43-61).  Importing ``reticulum_amd``
 itself never fails: its calls raise NativeUnavailable where the library or
 the device is missing (the batch API and the tests rely on that).
 """
-from ._native import available as _available
+from ._native import unavailable_reason as _unavailable_reason
 
-if not _available():
-    raise ImportError("reticulum_amd: librnstok.so or a gfx950 device is unavailable; "
-                      "use the reference implementation")
+_why = _unavailable_reason()
+if _why is not None:
+    raise ImportError("reticulum_amd: librnstok.so or a gfx950 device is unavailable (%s); "
+                      "use the reference implementation" % _why)
 
 from .hkdf import hkdf  # noqa: E402,F401
 from .token import AES, AES_128_CBC, AES_256_CBC, Token, TOKEN_OVERHEAD  # noqa: E402,F401

@@ -71,3 +71,55 @@ def test_swap_falls_back_to_reference_token_without_device():
         pytest.skip("a GPU is visible: the swap takes the HIP Token (tests/test_dropin_gpu.py)")
     which, mod = _run({})
     assert which == "reference" and mod == "RNS.Cryptography.Token"
+
+
+def _stub_library(tmp_path, drop=None, abi=None):
+    """A stand-in librnstok.so built from the binding table: every entry point
+    returns 0, `drop` is left out, rt_abi_version returns `abi`."""
+    from reticulum_amd import _native
+    lines = []
+    for name, _, _ in _native.SIGNATURES:
+        if name == drop:
+            continue
+        body = f"return {abi if abi is not None else _native.ABI_VERSION};" if name == "rt_abi_version" else "return 0;"
+        lines.append(f"long {name}(void) {{ {body} }}")
+    src = tmp_path / "stub.c"
+    src.write_text("\n".join(lines) + "\n")
+    so = tmp_path / "libstub.so"
+    subprocess.check_call(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)])
+    return str(so)
+
+
+def _dropin_outcome(lib):
+    env = dict(os.environ, RNSTOK_LIB=lib)
+    code = (f"import sys; sys.path.insert(0, {ROOT!r})\n"
+            "import reticulum_amd as rt\n"
+            "print('available', rt.available())\n"
+            "try:\n"
+            "    import reticulum_amd.dropin\n"
+            "    print('dropin imported')\n"
+            "except ImportError as e:\n"
+            "    print('ImportError', e)\n")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return r.stdout
+
+
+def test_dropin_import_fails_on_library_missing_a_symbol(tmp_path):
+    """a library older than the bindings (one entry point absent)
+    must read as unavailable, so the swap's `except ImportError` falls back,
+    instead of an AttributeError escaping the import."""
+    out = _dropin_outcome(_stub_library(tmp_path, drop="rt_clock_stamps"))
+    assert "available False" in out and "ImportError" in out and "older than these bindings" in out, out
+
+
+def test_dropin_import_fails_on_abi_version_mismatch(tmp_path):
+    out = _dropin_outcome(_stub_library(tmp_path, abi=1))
+    assert "available False" in out and "ImportError" in out and "ABI version 1" in out, out
+
+
+def test_available_false_on_bad_device_value():
+    env = dict(os.environ, RNSTOK_DEVICE="not-a-number")
+    r = subprocess.run([sys.executable, "-c", f"import sys; sys.path.insert(0, {ROOT!r}); import reticulum_amd as rt; "
+                        "print(rt.available())"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip() == "False", r.stderr[-2000:]

@@ -6,7 +6,8 @@
   and > 1000 ragged launches each, key sets created and destroyed per packet
   while another stream runs c2, a derived key set used right away from the
   host path, and the fused HKDF + key setup against the two-launch path.
-* Configs c3, c4 (general kernel) and c5 at BASELINE.json's full sizes:
+* Configs c3, c4 (general kernel) at BASELINE.json's full sizes and c5 at
+  its 8-GPU rank share (the whole c5 batch: tests/test_c5_full_gpu.py):
   size-independent properties (round trip, exact tamper set) plus seeded
   oracle samples of both directions.
 
@@ -328,8 +329,9 @@ def test_config_c4_full_size_general_kernel(rt):
     assert np.array_equal(ref, tok[s].cpu().numpy())
 
 
-def test_config_c5_full_size(rt):
-    """c5 on one GPU: 2^20 packets of 64-4096 B, 65 536 keys, half encrypted
+def test_config_c5_rank_share(rt):
+    """c5's per-rank share at 8 GPUs, on one GPU (the whole 8 M-packet batch
+    is tests/test_c5_full_gpu.py): 2^20 packets of 64-4096 B, 65 536 keys, half encrypted
     and half decrypted (length-bucketed launches), 1 % of the decrypt half
     tampered: exactly the tampered tokens fail with BAD_HMAC, every other
     plaintext round-trips, and seeded samples of the encrypt output and of

@@ -1505,9 +1505,16 @@ def c5_share_rate(dev, n_cu, n=1 << 20, steps=10, n_keys=65536, align=False):
             b.record(stream)
         torch.cuda.synchronize()
         ms = sorted(a.elapsed_time(b) for a, b in ev)[steps // 2]
+        # the kernels' own clock and cycles, from a stamped pass after the timed one
+        with device.LaunchClock(dev) as lc:
+            for _ in range(steps):
+                f()
+        clk = lc.summary().get(name, {})
         res[name] = {"ms": ms, "packets_s": (h if name == "encrypt" else n - h) / (ms * 1e-3),
                      "gib_s": bytes_ / (ms * 1e-3) / 2**30, "canonical_ops": o,
-                     "frac_of_valu_peak": o / (ms * 1e-3) / peak}
+                     "frac_of_valu_peak": o / (ms * 1e-3) / peak,
+                     "kernel_clock_ghz": clk.get("clock_ghz"), "kernel_cycles_per_launch": clk.get("cycles_per_launch"),
+                     "kernel_span_ms": clk.get("wg_span_ms")}
     tot = res["encrypt"]["ms"] + res["decrypt"]["ms"]
     res["packets_s"] = n / (tot * 1e-3)
     res["frac_of_valu_peak"] = (ops_e + ops_d) / (tot * 1e-3) / peak

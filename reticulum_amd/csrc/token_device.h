@@ -100,13 +100,15 @@ struct Lanes {
 // Address of the T-table row for byte k of state word s: {lane_off, s.byte_k, region, 0}.
 // Byte 1 is already in bits 8..15, so (s & 0xff00) | lane_off is one full-rate
 // v_bitop3; bytes 0, 2, 3 take one (half-rate) v_perm_b32.
-template <int K, int REGION>
+template <int K, int REGION, bool SHIFT = false>
 __device__ __forceinline__ uint32_t taddr(uint32_t s, const Lanes &L) {
     // (Bytes 0, 2, 3 by a shift to bits 8..15 plus the same and_or, two
     // dual-issuable ops instead of one v_perm, was 7-11 % slower on c2/c3 and
     // 14 % on the c4 shard: the kernels' mixed streams do not pair them,
-    // profiles/r03e_shift_addr_ab.txt.)
+    // profiles/r03e_shift_addr_ab.txt.  SHIFT keeps that form for the
+    // per-wave experiment of round 6.)
     if (K == 1) return and_or(s, L.m8, REGION ? L.r1 : L.r0);
+    if (SHIFT) return and_or(K == 0 ? s << 8 : s >> (8 * K - 8), L.m8, REGION ? L.r1 : L.r0);
     return perm(s, L.r1, REGION ? Sel<K>::R1 : Sel<K>::R0);
 }
 
@@ -122,15 +124,15 @@ __device__ __forceinline__ uint32_t tcol(uint32_t a, uint32_t b, uint32_t c, uin
 // their use: tround_load issues the 16 lookups, tround_mix folds them.
 // Column j reads bytes 0..3 of words (j, j+1, j+2, j+3) for encryption and
 // (j, j-1, j-2, j-3) for the equivalent inverse cipher.
-template <bool DEC>
+template <bool DEC, bool SHIFT = false>
 __device__ __forceinline__ void tround_load(uint32_t v[16], const uint32_t s[4], const Lanes &L) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int i1 = DEC ? (j + 3) & 3 : (j + 1) & 3, i2 = (j + 2) & 3, i3 = DEC ? (j + 1) & 3 : (j + 3) & 3;
-        v[4 * j + 0] = lds(taddr<0, 0>(s[j], L), 0);
-        v[4 * j + 1] = lds(taddr<1, 0>(s[i1], L), 128);
-        v[4 * j + 2] = lds(taddr<2, 1>(s[i2], L), 0);
-        v[4 * j + 3] = lds(taddr<3, 1>(s[i3], L), 128);
+        v[4 * j + 0] = lds(taddr<0, 0, SHIFT>(s[j], L), 0);
+        v[4 * j + 1] = lds(taddr<1, 0, SHIFT>(s[i1], L), 128);
+        v[4 * j + 2] = lds(taddr<2, 1, SHIFT>(s[i2], L), 0);
+        v[4 * j + 3] = lds(taddr<3, 1, SHIFT>(s[i3], L), 128);
     }
 }
 __device__ __forceinline__ void tround_mix(uint32_t s[4], const uint32_t v[16], const uint32_t *k) {
@@ -381,7 +383,7 @@ __device__ __forceinline__ void enc_quad(u32x4 c[4], const u32x4 x[4], u32x4 cha
 // equivalent inverse cipher with Td tables in regions 0/1:
 // t_j = Td0[s_j.b0] ^ Td1[s_{j-1}.b1] ^ Td2[s_{j-2}.b2] ^ Td3[s_{j-3}.b3] ^ dk_j,
 // SHA rounds of S interleaved when WITH_SHA.
-template <int NR, bool WITH_SHA>
+template <int NR, bool WITH_SHA, bool SHIFT = false>
 __device__ __forceinline__ void dec_quad(u32x4 p[4], const u32x4 c[4], u32x4 chain, const uint32_t *dk,
                                          const Lanes &L, Sha256 &S) {
     uint32_t s[4][4];
@@ -394,7 +396,7 @@ __device__ __forceinline__ void dec_quad(u32x4 p[4], const u32x4 c[4], u32x4 cha
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             uint32_t v[16];
-            tround_load<true>(v, s[b], L);
+            tround_load<true, SHIFT>(v, s[b], L);
             if (WITH_SHA) S.round((r - 1) * 4 + b);
             tround_mix(s[b], v, dk + 4 * r);
         }

@@ -47,6 +47,18 @@ namespace rnstok {
 #ifndef RNSTOK_DEC_ST_SC1            // decrypt: plaintext stores with sc1 (experiment)
 #define RNSTOK_DEC_ST_SC1 0
 #endif
+#ifndef RNSTOK_DEC_SHIFT_WAVES       // decrypt: per-wave full-rate address experiment (bit mask of wave slots)
+#define RNSTOK_DEC_SHIFT_WAVES 0
+#endif
+#ifndef RNSTOK_ENC_ST_SECTOR         // split encrypt: ciphertext stores grouped by 64-B sector
+#define RNSTOK_ENC_ST_SECTOR 1
+#endif
+#ifndef RNSTOK_ENC_ST_SECTOR_PERKEY  // the same for per-packet keys (experiment)
+#define RNSTOK_ENC_ST_SECTOR_PERKEY 0
+#endif
+#ifndef RNSTOK_ENC_PAIR_PERKEY       // per-packet keys: plaintext quads loaded in pairs
+#define RNSTOK_ENC_PAIR_PERKEY RNSTOK_ENC_PAIR
+#endif
 #ifndef RNSTOK_SPLIT_DYN              // split encrypt: unevenly divided uniform batches from a counter
 #define RNSTOK_SPLIT_DYN 1
 #endif
@@ -515,14 +527,22 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
             const uint8_t *P = pt_at(p);
             uint8_t *O = tok_at(p);
             u32x4 prev = valid ? ld16(a.iv + 16ull * p) : z;
-            if (valid) st16(O, prev);
             uint8_t *C = O + US;
+            // RNSTOK_ENC_ST_SECTOR (experiment): the ciphertext units of a 64-B
+            // sector that a quad shares with the next are stored together with
+            // the next quad's, so every sector is written by back-to-back stores
+            // (sg: the sector phase of the lane's ciphertext start, in units)
+            constexpr bool SECT = !ILV && (PERKEY ? RNSTOK_ENC_ST_SECTOR_PERKEY : RNSTOK_ENC_ST_SECTOR);
+            // (lane 0 stores at once: its hashing lane reads the quad back from the token buffer)
+            const uint32_t sg = SECT && lane ? ((uint32_t)(uintptr_t)C >> 4) & 3u : 0u;
+            u32x4 cp1 = z, cp2 = z;                        // the previous quad's units 1, 2 (unit 3: prev)
+            if (valid && (!SECT || sg == 0u)) st16(O, prev);
             // (experiment, RNSTOK_SPLIT_TILE: packed batches whose plaintexts a
             // gather pass laid out as 64-packet tiles, unit u of lane l at
             // pt_off + 1024 u; tokens stay byte strings)
             const uint64_t USP = GEN && RNSTOK_SPLIT_TILE ? 1024ull : US;
             // packed rows: full quads loaded in line-sharing pairs (k_decrypt)
-            constexpr bool PAIR = RNSTOK_ENC_PAIR && !ILV;
+            constexpr bool PAIR = (PERKEY ? RNSTOK_ENC_PAIR_PERKEY : RNSTOK_ENC_PAIR) && !ILV;
             u32x4 nx[4];
             for (uint32_t q = 0; q <= wq; ++q) {
                 u32x4 x[4], c[4];
@@ -546,7 +566,23 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_encrypt_split(EncArgs a) {
                 }
                 enc_quad<NR, false>(c, x, prev, K.rk, LN, S);
                 const uint32_t nst = q < nq ? 4u : tb;
-                if (act) {
+                if (SECT) {
+                    if (act) {
+                        if (q == 0u) {
+                            if (sg != 0u) st16(C - US, prev);            // the IV, with its sector's units
+                        } else {                                         // the previous quad's held units
+                            if (sg == 3u) st16(C - 3 * US, cp1);
+                            if (sg >= 2u) st16(C - 2 * US, cp2);
+                            if (sg >= 1u) st16(C - US, prev);
+                        }
+                        const uint32_t now = q == nq ? nst : (4u - sg < nst ? 4u - sg : nst);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if ((uint32_t)j < now) st16(C + US * j, c[j]);
+                    }
+                    cp1 = c[1];
+                    cp2 = c[2];
+                } else if (act) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
                         if ((uint32_t)j < nst) st16(C + US * j, c[j]);
@@ -1138,6 +1174,14 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
                 // (the touch's register is released only after a later load's
                 // data was waited for: vmcnt counts in issue order)
                 if (RNSTOK_DEC_TOUCH >= 2 && PAIR && !(q & 1u)) asm volatile("" ::"v"(touch));
+#if RNSTOK_DEC_SHIFT_WAVES
+                // experiment (round 6): the waves in the slots of RNSTOK_DEC_SHIFT_WAVES
+                // (bit k: the (k+1)-th wave of each SIMD) build T-table addresses from
+                // full-rate shift + bitop3 instead of v_perm
+                if (!PERKEY && !ILV && ((RNSTOK_DEC_SHIFT_WAVES >> (threadIdx.x >> 8)) & 1))
+                    dec_quad<NR, true, true>(pp, c, prev, K.rk, LN, S);
+                else
+#endif
                 dec_quad<NR, true>(pp, c, prev, K.rk, LN, S);
 #pragma unroll
                 for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(S.v[k]));   // see k_encrypt

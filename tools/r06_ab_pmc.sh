@@ -18,7 +18,8 @@ grep -v amdgpu.ids $O/ab.txt
 [ -n "$NO_PMC" ] && exit 0
 BASE="--steps 30 --warmup 2 --cpu-seconds 0 --no-e2e --no-node --one-layout --no-aligned $BENCH_ARGS"
 for v in "$@"; do
-  for PASS in "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+  IFS=';' read -ra PS <<< "${PMC_PASSES:-FETCH_SIZE;WRITE_SIZE;GRBM_GUI_ACTIVE GRBM_COUNT}"
+  for PASS in "${PS[@]}"; do
     N=$(echo $PASS | tr ' ' '_' | cut -c1-40)
     RNSTOK_LIB=exp_ship/$v/librnstok.so timeout -s KILL 120 rocprofv3 --pmc $PASS --output-format csv -d $O/${v}_$N -o run \
       -- python3 bench.py $BASE > $O/${v}_$N.log 2>&1 || { echo "pmc $v $N failed rc=$?"; tail -5 $O/${v}_$N.log; exit 1; }

@@ -49,10 +49,15 @@ def main():
     for k in ("encrypt", "decrypt"):
         print(k)
         for v in vs:
+            v_name = v
             m = res[v].get(k, {})
             print("  %-10s fetch %8.3f GB  write %8.3f GB  traffic %6.3f GB (%.2fx)  GRBM_GUI_ACTIVE %10.0f" % (
                 v, 2 * m.get("FETCH_SIZE", 0) * 1024 / 1e9, m.get("WRITE_SIZE", 0) * 1024 / 1e9,
                 m.get("traffic_gb", 0), m.get("traffic_x", 0), m.get("GRBM_GUI_ACTIVE", 0)))
+            if "SQ_INSTS_VALU" in m:
+                v, v2 = m["SQ_INSTS_VALU"], m.get("SQ_ACTIVE_INST_VALU2", 0)
+                print("  %-10s VALU %.4g  VALU2 %.4g (dual-issued %.1f %%)  LDS %.4g  issue slots (VALU-VALU2+LDS) %.4g" % (
+                    v_name, v, v2, 200 * v2 / v, m.get("SQ_INSTS_LDS", 0), v - v2 + m.get("SQ_INSTS_LDS", 0)))
     with open(os.path.join(root, "pmc_cmp.json"), "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
 

@@ -50,14 +50,23 @@ namespace rnstok {
 #ifndef RNSTOK_DEC_SHIFT_WAVES       // decrypt: per-wave full-rate address experiment (bit mask of wave slots)
 #define RNSTOK_DEC_SHIFT_WAVES 0
 #endif
-#ifndef RNSTOK_ENC_ST_SECTOR         // split encrypt: ciphertext stores grouped by 64-B sector
+// Split encrypt, packed rows: the ciphertext units of a 64-B sector that a quad
+// shares with the next quad are held and stored with the next quad's, so every
+// sector leaves in one burst of stores (fabric write requests 18.3 M -> 12.8 M
+// per c2 launch, the count of the same tokens with their ciphertext on lines).
+// The chip then holds a higher clock: whole-bench A/Bs (each variant its own
+// sustained run) c2 +2.2 % (2.20 -> 2.25 GHz, cycles equal), per-packet keys
+// c3 encrypt -2.9 %, c5's encrypt half -4.7 % (profiles/r06_clock_ab/).  An A/B
+// that interleaves the variants launch by launch shares one clock between
+// them and showed +1.3 %.
+#ifndef RNSTOK_ENC_ST_SECTOR
 #define RNSTOK_ENC_ST_SECTOR 1
 #endif
-#ifndef RNSTOK_ENC_ST_SECTOR_PERKEY  // the same for per-packet keys (experiment)
-#define RNSTOK_ENC_ST_SECTOR_PERKEY 0
+#ifndef RNSTOK_ENC_ST_SECTOR_PERKEY  // per-packet keys: with single plaintext quads (next line) 5 VGPRs
+#define RNSTOK_ENC_ST_SECTOR_PERKEY 1  // spilled; with the paired loads 31
 #endif
-#ifndef RNSTOK_ENC_PAIR_PERKEY       // per-packet keys: plaintext quads loaded in pairs
-#define RNSTOK_ENC_PAIR_PERKEY RNSTOK_ENC_PAIR
+#ifndef RNSTOK_ENC_PAIR_PERKEY       // per-packet keys: plaintext quads loaded in pairs (off: the
+#define RNSTOK_ENC_PAIR_PERKEY 0     // registers go to the held sector units)
 #endif
 #ifndef RNSTOK_SPLIT_DYN              // split encrypt: unevenly divided uniform batches from a counter
 #define RNSTOK_SPLIT_DYN 1

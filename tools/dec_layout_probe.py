@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--length", type=int, default=500)
     ap.add_argument("--kernel", choices=["decrypt", "encrypt"], default="decrypt")
     ap.add_argument("--back-stride", type=int, default=0, help="decrypt output row stride (0: tl - 48)")
+    ap.add_argument("--pt-stride", type=int, default=0, help="encrypt input row stride (0: packed, the length)")
     ap.add_argument("--extra", default="", help="more token layouts, e.g. 576+0,640+0 (stride+first offset)")
     args = ap.parse_args()
     import torch
@@ -32,7 +33,10 @@ def main():
     tl = rt.token_len(L)
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(3)
-    pt = torch.randint(0, 256, (n, L), dtype=torch.uint8, device=dev, generator=g)
+    ps = args.pt_stride or L
+    pt_buf = torch.empty(n * ps + 256, dtype=torch.uint8, device=dev)
+    pt = pt_buf[(-pt_buf.data_ptr()) % 256:].as_strided((n, L), (ps, 1))
+    pt.copy_(torch.randint(0, 256, (n, L), dtype=torch.uint8, device=dev, generator=g))
     iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device=dev, generator=g)
     ks = rt.KeySet(os.urandom(64), device=0)
     def rows(stride, off):
@@ -86,7 +90,7 @@ def main():
             res[name]["cycles"].append(c["cycles_per_launch"])
     out = {k: {"ms": statistics.median(v["ms"]), "clock_ghz": statistics.median(v["clock"]),
                "cycles_per_launch": statistics.median(v["cycles"])} for k, v in res.items()}
-    out["workload"] = {"packets": n, "length": L, "kernel": args.kernel, "back_stride": bs}
+    out["workload"] = {"packets": n, "length": L, "kernel": args.kernel, "back_stride": bs, "pt_stride": ps}
     print(json.dumps(out))
 
 

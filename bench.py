@@ -1434,32 +1434,36 @@ def c5_share_rate(dev, n_cu, n=1 << 20, steps=10, n_keys=65536, align=False):
     h = n // 2
     le, ld = lens[:h].to(dev), lens[h:].to(dev)
 
-    def offs(x, phase=0):
+    # align: True (every buffer) or a set of "enc_in", "enc_out", "dec_in", "dec_out"
+    sides = {"enc_in", "enc_out", "dec_in", "dec_out"} if align is True else set(align or ())
+
+    def offs(x, phase=0, side=None):
+        al = side in sides
         w = x.to(torch.int64)
-        if align:
+        if al:
             w = (w + 127) // 128 * 128
         o = torch.zeros(x.numel(), dtype=torch.int64, device=dev)
         o[1:] = torch.cumsum(w[:-1], 0)
-        return o + ((-phase) % 128 if align else 0)
+        return o + ((-phase) % 128 if al else 0)
 
     def span(o, x):
         return int(o[-1]) + int(x[-1]) + 1
 
     tlen = lambda x: (16 + 16 * (x // 16 + 1) + 32).to(torch.int32)     # noqa: E731
     # encrypt half: plaintexts -> tokens
-    oe, ive = offs(le), torch.randint(0, 256, (h, 16), dtype=torch.uint8, device=dev, generator=g)
+    oe, ive = offs(le, 0, "enc_in"), torch.randint(0, 256, (h, 16), dtype=torch.uint8, device=dev, generator=g)
     pe = torch.randint(0, 256, (span(oe, le),), dtype=torch.uint8, device=dev, generator=g)
     te_len = tlen(le)
-    te_off = offs(te_len, 16)
+    te_off = offs(te_len, 16, "enc_out")
     te = torch.empty(span(te_off, te_len), dtype=torch.uint8, device=dev)
     # decrypt half: tokens made before timing
     od, ivd = offs(ld), torch.randint(0, 256, (n - h, 16), dtype=torch.uint8, device=dev, generator=g)
     pd = torch.randint(0, 256, (span(od, ld),), dtype=torch.uint8, device=dev, generator=g)
     td_len = tlen(ld)
-    td_off = offs(td_len, 16)
+    td_off = offs(td_len, 16, "dec_in")
     td = torch.empty(span(td_off, td_len), dtype=torch.uint8, device=dev)
     device.encrypt(ks, pd, od, ld, ivd, td, td_off, key_idx=kidx[h:], sort=True)
-    boff = offs(td_len - 48)
+    boff = offs(td_len - 48, 0, "dec_out")
     back = torch.empty(span(boff, td_len - 48), dtype=torch.uint8, device=dev)
     ol = torch.empty(n - h, dtype=torch.int32, device=dev)
     st = torch.empty(n - h, dtype=torch.int32, device=dev)
@@ -1472,7 +1476,7 @@ def c5_share_rate(dev, n_cu, n=1 << 20, steps=10, n_keys=65536, align=False):
     torch.cuda.synchronize()
     ok = bool((st == 0).all()) and torch.equal(ol, ld)
     # round trip of a sample of the encrypt half's tokens, and the decrypt half's plaintexts
-    coff = offs(te_len - 48)
+    coff = offs(te_len - 48, 0, "enc_in")
     chk = torch.empty(span(coff, te_len - 48), dtype=torch.uint8, device=dev)
     cl = torch.empty(h, dtype=torch.int32, device=dev)
     cs = torch.empty(h, dtype=torch.int32, device=dev)
@@ -1494,8 +1498,9 @@ def c5_share_rate(dev, n_cu, n=1 << 20, steps=10, n_keys=65536, align=False):
     peak = n_cu * 128 * 2.4e9
     res = {"packets": n, "keys": n_keys, "encrypt_packets": h, "decrypt_packets": n - h,
            "plaintext_bytes": int(L64.sum()), "mean_plaintext_bytes": float(L64.float().mean()), "ok": ok,
-           "layout": ("byte strings in 128-B-aligned slots (prefix sums of whole lines)" if align else
-                      "packed rows (byte strings at prefix-sum offsets)") + ", length-bucketed on the device"}
+           "layout": (("byte strings in 128-B-aligned slots (prefix sums of whole lines)" if align is True else
+                       "byte strings in 128-B-aligned slots for " + ",".join(sorted(sides)) + ", packed elsewhere")
+                      if sides else "packed rows (byte strings at prefix-sum offsets)") + ", length-bucketed on the device"}
     for name, f, o, bytes_ in (("encrypt", enc, ops_e, int(L64[:h].sum())), ("decrypt", dec, ops_d, int(L64[h:].sum()))):
         warmup(f, stream, 2, 0.3)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]

@@ -74,11 +74,6 @@ __device__ __forceinline__ u32x4 ld16(const uint8_t *p) {
     return v;
 }
 __device__ __forceinline__ void st16(uint8_t *p, u32x4 v) { __builtin_memcpy(p, &v, 16); }
-// 16-B store with the sc1 cache policy (written through, line not kept in L2).
-// The s_nop covers the >8-B store-data hazard the compiler does not see in asm.
-__device__ __forceinline__ void st16_sc1(uint8_t *p, u32x4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-}
 
 // Per-lane constants for LDS addressing; lane l always hits bank (l & 31).
 // A VALU op that reads an SGPR (or a constant materialised in one) issues at

@@ -44,8 +44,11 @@ namespace rnstok {
 #ifndef RNSTOK_DEC_TAG_LAST          // decrypt: tag units loaded at the start of the last quad
 #define RNSTOK_DEC_TAG_LAST 0
 #endif
-#ifndef RNSTOK_DEC_ST_SC1            // decrypt: plaintext stores with sc1 (experiment)
-#define RNSTOK_DEC_ST_SC1 0
+#ifndef RNSTOK_DEC_ST_SECTOR         // decrypt: plaintext stores grouped by 64-B sector (experiment)
+#define RNSTOK_DEC_ST_SECTOR 0
+#endif
+#ifndef RNSTOK_DEC_ST_SECTOR_PERKEY
+#define RNSTOK_DEC_ST_SECTOR_PERKEY 0
 #endif
 #ifndef RNSTOK_DEC_SHIFT_WAVES       // decrypt: per-wave full-rate address experiment (bit mask of wave slots)
 #define RNSTOK_DEC_SHIFT_WAVES 0
@@ -1146,6 +1149,12 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
             constexpr bool PAIR = RNSTOK_DEC_PAIR && !ILV && !PERKEY && WG <= 768;   // (1024: 11 -> 38 VGPRs spilled)
             u32x4 nx[4];
             uint32_t touch = 0u;
+            // RNSTOK_DEC_ST_SECTOR (experiment): plaintext stores grouped by 64-B
+            // sector, as k_encrypt_split's ciphertext stores (dsg: the sector
+            // phase of the lane's output, in units; 0 = every quad on a sector)
+            constexpr bool DSECT = !ILV && (PERKEY ? RNSTOK_DEC_ST_SECTOR_PERKEY : RNSTOK_DEC_ST_SECTOR);
+            const uint32_t dsg = DSECT ? ((uint32_t)(uintptr_t)O >> 4) & 3u : 0u;
+            u32x4 hp1 = z, hp2 = z, hp3 = z;
 #pragma nounroll
             for (uint32_t q = 0; q <= nq; ++q) {
                 const uint32_t nbk = q < nq ? 4u : tb;
@@ -1197,18 +1206,23 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
                 const bool keep = nbk >= 3u;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) h[k] += keep ? S.v[k] : 0u;
-#if RNSTOK_DEC_ST_SC1
-                // experiment: write-through stores that drop their line from L2
-                // (MI355X_MICROARCH.md: sc1 stores do not keep the line), so
-                // the L2 holds the token lines the next pair shares
-                if (!ILV && !PERKEY) {
-                    st16_sc1(D, pp[0]);
-                    if (nbk > 1u) st16_sc1(D + US, pp[1]);
-                    if (nbk > 2u) st16_sc1(D + 2 * US, pp[2]);
-                    if (nbk > 3u) st16_sc1(D + 3 * US, pp[3]);
-                } else
-#endif
-                {
+                if (DSECT) {
+                    // the held units of the previous quad's last sector, then this
+                    // quad's units up to its first sector boundary (all at the tail)
+                    if (q != 0u) {
+                        if (dsg == 3u) st16(D - 3 * US, hp1);
+                        if (dsg >= 2u) st16(D - 2 * US, hp2);
+                        if (dsg >= 1u) st16(D - US, hp3);
+                    }
+                    const uint32_t now = q == nq ? nbk : (4u - dsg < nbk ? 4u - dsg : nbk);
+                    st16(D, pp[0]);
+                    if (now > 1u) st16(D + US, pp[1]);
+                    if (now > 2u) st16(D + 2 * US, pp[2]);
+                    if (now > 3u) st16(D + 3 * US, pp[3]);
+                    hp1 = pp[1];
+                    hp2 = pp[2];
+                    hp3 = pp[3];
+                } else {
                     st16(D, pp[0]);
                     if (nbk > 1u) st16(D + US, pp[1]);
                     if (nbk > 2u) st16(D + 2 * US, pp[2]);

@@ -183,3 +183,104 @@ def test_split_kernel_packed_batches(rt, sort, n_keys, lo, hi):
     for i in sel:
         want = oracle.encrypt(keys[kx[i]].tobytes(), iv_h[i].tobytes(), p_h[off[i]:off[i] + lens[i]].tobytes())
         assert t_h[toff[i]:toff[i] + tl[i]].tobytes() == want, i
+
+
+@pytest.mark.parametrize("L,extra_stride,base_off,n_keys", [(500, 0, 16, 1), (500, 16, 0, 1), (500, 32, 48, 1),
+                                                            (500, 48, 32, 1), (17, 16, 16, 1), (47, 48, 0, 1),
+                                                            (1500, 32, 16, 1), (383, 16, 48, 97), (0, 0, 32, 1),
+                                                            (64, 16, 0, 65536)])
+def test_split_sector_grouped_stores_every_phase(rt, L, extra_stride, base_off, n_keys):
+    """k_encrypt_split stores each 64-B sector of ciphertext in one burst, holding
+    the units a quad shares with the next (round 6).  Token rows at strides and
+    first offsets that put the IV and every quad at each of the four sector
+    phases, into a sentinel-filled buffer: every token equal to the interleaved
+    layout's (which stores whole quads) and a sample to the oracle, and no byte
+    between the rows written."""
+    import torch
+    from reticulum_amd import _native, device
+    n = _split_n(5)
+    lib, ctx = _native.load(), _native.context(0)
+    tl = rt.token_len(L)
+    assert lib.rt_plan_uniform(ctx, n, L, int(n_keys > 1), 0) == _native.RT_KERNEL_ENC_SPLIT
+    rng = np.random.Generator(np.random.PCG64(77 + L + extra_stride + base_off))
+    keys = rng.integers(0, 256, (n_keys, 64), dtype=np.uint8)
+    ks = rt.KeySet(keys if n_keys > 1 else keys[0].tobytes())
+    kidx = torch.from_numpy(rng.integers(0, n_keys, n).astype(np.int32)).cuda() if n_keys > 1 else None
+    g = torch.Generator(device="cuda").manual_seed(L + 11)
+    pt = torch.randint(0, 256, (n, max(L, 1)), dtype=torch.uint8, device="cuda", generator=g)[:, :L]
+    iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
+    ts = tl + extra_stride
+    buf = torch.full((n * ts + 256,), 0xEE, dtype=torch.uint8, device="cuda")
+    base = (-buf.data_ptr()) % 64 + base_off
+    tok = buf[base:].as_strided((n, tl), (ts, 1))
+    device.encrypt_uniform(ks, pt, L, iv, tok, key_idx=kidx)
+    tu = torch.full((tl // 16, n, 16), 0xEE, dtype=torch.uint8, device="cuda")
+    device.encrypt_interleaved(ks, device.interleave(pt, L), L, iv, tu, key_idx=kidx)
+    torch.cuda.synchronize()
+    assert torch.equal(device.deinterleave(tu, tl), tok)
+    # the gaps between rows and the bytes around the batch stay untouched
+    mask = torch.ones(buf.numel(), dtype=torch.bool, device="cuda")
+    rows = (base + torch.arange(n, device="cuda", dtype=torch.int64)[:, None] * ts
+            + torch.arange(tl, device="cuda", dtype=torch.int64)[None, :]).reshape(-1)
+    mask[rows] = False
+    assert bool((buf[mask] == 0xEE).all())
+    t_h, p_h, iv_h = tok.cpu().numpy(), pt.cpu().numpy(), iv.cpu().numpy()
+    kx = kidx.cpu().numpy() if kidx is not None else np.zeros(n, np.int64)
+    for i in np.unique(np.concatenate([[0, 1, 2, 3, 63, 64, n - 1], rng.integers(0, n, 24)])):
+        assert t_h[i].tobytes() == oracle.encrypt(keys[kx[i]].tobytes(), iv_h[i].tobytes(), p_h[i].tobytes()), i
+
+
+@pytest.mark.parametrize("n_keys", [1, 65536])
+def test_split_sector_grouped_stores_packed_length_ordered(rt, n_keys):
+    """The length-ordered packed path (c5's encrypt half) with sector-grouped
+    stores: tokens at prefix-sum offsets from a 16-B-misaligned first one, into a
+    sentinel-filled buffer; every token round-trips, a sample equals the oracle,
+    and no byte outside the tokens is written."""
+    import torch
+    from reticulum_amd import _native, device
+    n = _split_n(3)
+    rng = np.random.Generator(np.random.PCG64(4242 + n_keys))
+    keys = rng.integers(0, 256, (n_keys, 64), dtype=np.uint8)
+    ks = rt.KeySet(keys if n_keys > 1 else keys[0].tobytes())
+    kidx = torch.from_numpy(rng.integers(0, n_keys, n).astype(np.int32)).cuda() if n_keys > 1 else None
+    lens = rng.integers(0, 700, n).astype(np.int32)
+    off = np.zeros(n, np.int64)
+    off[1:] = np.cumsum(lens[:-1])
+    tl = (16 + 16 * (lens // 16 + 1) + 32).astype(np.int64)
+    toff = np.zeros(n, np.int64)
+    toff[1:] = np.cumsum(tl[:-1])
+    toff += 48
+    cu = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    g = torch.Generator(device="cuda").manual_seed(99)
+    buf = torch.randint(0, 256, (int(lens.astype(np.int64).sum()) + 1,), dtype=torch.uint8, device="cuda", generator=g)
+    iv = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
+    tok = torch.full((int(toff[-1] + tl[-1]) + 64,), 0xEE, dtype=torch.uint8, device="cuda")
+    ws = torch.empty(int(_native.load().rt_workspace_bytes(n)), dtype=torch.uint8, device="cuda")
+    device.encrypt(ks, buf, cu(off), cu(lens), iv, tok, cu(toff), key_idx=kidx, sort=True, workspace=ws)
+    torch.cuda.synchronize()
+    th = tok.cpu().numpy()
+    covered = np.zeros(th.size, bool)
+    starts, ends = toff, toff + tl
+    d = np.zeros(th.size + 1, np.int64)
+    np.add.at(d, starts, 1)
+    np.add.at(d, ends, -1)
+    covered = np.cumsum(d)[:-1] > 0
+    assert (th[~covered] == 0xEE).all()
+    cap = tl - 48
+    coff = np.zeros(n, np.int64)
+    coff[1:] = np.cumsum(cap[:-1])
+    back = torch.zeros(int(cap.sum()), dtype=torch.uint8, device="cuda")
+    ol = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    device.decrypt(ks, tok, cu(toff), cu(tl.astype(np.int32)), back, cu(coff), ol, st, key_idx=kidx, sort=True,
+                   workspace=ws)
+    torch.cuda.synchronize()
+    assert bool((st == 0).all()) and np.array_equal(ol.cpu().numpy(), lens)
+    hb, hiv, hback = buf.cpu().numpy(), iv.cpu().numpy(), back.cpu().numpy()
+    kx = kidx.cpu().numpy() if kidx is not None else np.zeros(n, np.int64)
+    for i in rng.integers(0, n, 300):
+        p = hb[off[i]:off[i] + lens[i]].tobytes()
+        assert hback[coff[i]:coff[i] + lens[i]].tobytes() == p, i
+    for i in rng.integers(0, n, 48):
+        p = hb[off[i]:off[i] + lens[i]].tobytes()
+        assert th[toff[i]:toff[i] + tl[i]].tobytes() == oracle.encrypt(keys[kx[i]].tobytes(), hiv[i].tobytes(), p), i

@@ -38,12 +38,6 @@ namespace rnstok {
 #ifndef RNSTOK_DEC_PAIR              // decrypt, one key, token quads loaded in pairs: fetch -21 %, time -1.6 %
 #define RNSTOK_DEC_PAIR 1
 #endif
-#ifndef RNSTOK_DEC_TOUCH             // decrypt pairs: odd quads touch the next pair's first line in L2
-#define RNSTOK_DEC_TOUCH 0
-#endif
-#ifndef RNSTOK_DEC_TAG_LAST          // decrypt: tag units loaded at the start of the last quad
-#define RNSTOK_DEC_TAG_LAST 0
-#endif
 #ifndef RNSTOK_DEC_ST_SECTOR         // decrypt: plaintext stores grouped by 64-B sector (experiment)
 #define RNSTOK_DEC_ST_SECTOR 0
 #endif
@@ -1131,8 +1125,7 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
             u32x4 prev = ld16(Kt);
             // (RNSTOK_DEC_TAG_EARLY: the tag's two units loaded before the quad
             // loop, so the compare after it does not wait on them)
-            constexpr bool TAG_LAST = RNSTOK_DEC_TAG_LAST && !ILV && !PERKEY && WG <= 768;
-            constexpr bool TAG_EARLY = RNSTOK_DEC_TAG_EARLY && !TAG_LAST && !PERKEY && WG <= 768;
+            constexpr bool TAG_EARLY = RNSTOK_DEC_TAG_EARLY && !PERKEY && WG <= 768;
             u32x4 tag0, tag1;
             if (TAG_EARLY) {
                 tag0 = ld16(Kt + US * ((T >> 4) - 2u));
@@ -1148,7 +1141,6 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
             // L2 through and the line is fetched again: 2.7x read traffic)
             constexpr bool PAIR = RNSTOK_DEC_PAIR && !ILV && !PERKEY && WG <= 768;   // (1024: 11 -> 38 VGPRs spilled)
             u32x4 nx[4];
-            uint32_t touch = 0u;
             // RNSTOK_DEC_ST_SECTOR (experiment): plaintext stores grouped by 64-B
             // sector, as k_encrypt_split's ciphertext stores (dsg: the sector
             // phase of the lane's output, in units; 0 = every quad on a sector)
@@ -1158,22 +1150,9 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
 #pragma nounroll
             for (uint32_t q = 0; q <= nq; ++q) {
                 const uint32_t nbk = q < nq ? 4u : tb;
-                if (TAG_LAST && q == nq) {
-                    tag0 = ld16(Kt + US * ((T >> 4) - 2u));
-                    tag1 = ld16(Kt + US * ((T >> 4) - 1u));
-                }
                 if (PAIR && (q & 1u)) {
 #pragma unroll
                     for (int k = 0; k < 4; ++k) c[k] = nx[k];
-                    // the next pair's first unit usually shares a 128-B line
-                    // with this pair's last; an L2-served touch one quad
-                    // before it is needed keeps the line from being evicted
-                    if (RNSTOK_DEC_TOUCH == 1 && q < nq)
-                        (void)*(volatile const __attribute__((address_space(1))) uint32_t *)(uintptr_t)(C + 4 * US);
-                    if (RNSTOK_DEC_TOUCH == 2 && q < nq)
-                        touch = __hip_atomic_load((const uint32_t *)(C + 4 * US), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (RNSTOK_DEC_TOUCH == 3 && q < nq)
-                        asm volatile("global_load_dword %0, %1, off" : "=v"(touch) : "v"(C + 4 * US) : "memory");
                 } else {
                     c[0] = ld16(C);
                     c[1] = nbk > 1u ? ld16(C + US) : z;
@@ -1189,9 +1168,6 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
                 }
                 S.start(h);
                 sha_units(S.w, prev, c[0], c[1], c[2]);
-                // (the touch's register is released only after a later load's
-                // data was waited for: vmcnt counts in issue order)
-                if (RNSTOK_DEC_TOUCH >= 2 && PAIR && !(q & 1u)) asm volatile("" ::"v"(touch));
 #if RNSTOK_DEC_SHIFT_WAVES
                 // experiment (round 6): the waves in the slots of RNSTOK_DEC_SHIFT_WAVES
                 // (bit k: the (k+1)-th wave of each SIMD) build T-table addresses from
@@ -1236,7 +1212,7 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
             // pp[0..tb-1] its plaintext
             const u32x4 pb = ld16(Kt + 4ull * US * nq);
             u32x4 r0, r1;
-            if (TAG_EARLY || TAG_LAST) {
+            if (TAG_EARLY) {
                 r0 = tag0;
                 r1 = tag1;
             } else {

@@ -517,7 +517,8 @@ def main():
         },
         "roofline": {"bound": "valu", "kernel": dom, "achieved": achieved / 1e12, "peak": peak_valu / 1e12,
                      "unit": "TOP/s", "frac": achieved / peak_valu,
-                     "traffic": (traffic or {}).get("bytes_with_x2_fetch_correction"),
+                     "traffic": (traffic or {}).get("bytes_calibrated") or (traffic or {}).get("bytes_with_x2_fetch_correction"),
+                     "traffic_guide_x2": (traffic or {}).get("bytes_with_x2_fetch_correction"),
                      "traffic_detail": traffic,
                      "ops_per_packet": ops_dec(L) if dom == "decrypt" else ops_enc(L),
                      "algorithmic_bytes_per_launch": hbm_bytes,
@@ -541,13 +542,15 @@ def main():
                              "clock_ghz / cycles_per_launch / frac_at_measured_clock are measured in THIS run: every "
                              "workgroup of the timed launches stamps its span in shader cycles and 100 MHz ticks "
                              "(rt_clock_stamps; in_run_clock has both kernels); sustained_clock_ghz_committed_pmc is "
-                             "the builder's PMC run (GRBM_GUI_ACTIVE / 8 XCDs / kernel-trace average); ceiling_frac = the "
+                             "the builder's PMC run (GRBM_GUI_ACTIVE / 8 XCDs / kernel-trace average); traffic = HBM bytes per launch from "
+                             "the committed PMC with FETCH_SIZE scaled by a pure-read calibration of the kernel's own "
+                             "read pattern where one exists (traffic_detail.fetch_calibration; the guide's x2 streaming "
+                             "correction, traffic_guide_x2, overstates packed rows' sector-sized requests); ceiling_frac = the "
                              "guide-peak fraction this instruction stream reaches at most (its ISA slot floor: every "
                              "dual-issuable op paired, every LDS lookup a slot), ceiling_frac_valu_only the same with "
                              "every lookup hidden behind other waves' VALU issue; frac_over_ceiling = frac / "
-                             "ceiling_frac (DESIGN.md §4.5); traffic = HBM "
-                             "bytes per launch from the committed rocprofv3 PMC summary (profiles/*_pmc.json, FETCH_SIZE "
-                             "x 2 + WRITE_SIZE; see traffic_detail.calibration). issue_model = the kernel's issue slots "
+                             "ceiling_frac (DESIGN.md §4.5, §4.10); the PMC summary is the newest committed "
+                             "profiles/*_pmc.json of this workload (traffic_detail.source). issue_model = the kernel's issue slots "
                              "from its ISA (floor: every dual-issuable op paired; ceiling: none), its issued slots from "
                              "the PMC (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2 + SQ_INSTS_LDS), and measured_core = the "
                              "kernel's own compute core timed from registers (tools/floor_probe.hip); DESIGN.md §4.5"},
@@ -1123,6 +1126,20 @@ def sustained_clock_ghz(kernel, n, L, keys, layout="rows"):
         return None
 
 
+# FETCH_SIZE scale per kernel read pattern, from a pure-read kernel over known
+# bytes in the same pattern (MI355X_MICROARCH.md §HBM: "calibrate on a known
+# byte count in your own access pattern"; tools/fetch_calib.sh,
+# profiles/r06_fetch_calib.txt): packed c2 token rows read as k_decrypt reads
+# them report 548.1 MB for 587.2 MB (a mix of 64-B and 128-B requests, each
+# tallied at 64 B), so their bytes are FETCH_SIZE x 1.071; the guide's x2 holds
+# for whole-line streams (the interleaved layout, tokens with their ciphertext
+# on lines: 0.684 x).
+FETCH_CALIBRATION = {
+    ("decrypt", "rows"): (587.2 / 548.1, "FETCH_SIZE x 1.071: packed 560-B token rows read in 8-unit groups, "
+                                         "548.1 MB counted for 587.2 MB known (profiles/r06_fetch_calib.txt)"),
+}
+
+
 def traffic_from_profiles(kernel, n, L, keys, layout="rows"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     whose workload matches (profiles/<round>_pmc.json, tools/pmc_summary.py)."""
@@ -1130,14 +1147,20 @@ def traffic_from_profiles(kernel, n, L, keys, layout="rows"):
     if path:
         raw = d[kernel].get("hbm_bytes_per_launch_uncorrected")
         if raw:
+            m = d[kernel]
+            k = FETCH_CALIBRATION.get((kernel, layout))
+            cal = (k[0] * m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024 if k and "FETCH_SIZE" in m and "WRITE_SIZE" in m else None
             return {"bytes": raw, "bytes_with_x2_fetch_correction": d[kernel].get("hbm_bytes_per_launch"),
+                    "bytes_calibrated": cal, "fetch_calibration": k[1] if k else None,
                     "source": os.path.relpath(path, ROOT),
-                    "calibration": "roofline.traffic = FETCH_SIZE x 2 + WRITE_SIZE (the guide's gfx950 correction); bytes = "
-                                   "FETCH_SIZE + WRITE_SIZE as counted. The x2 FETCH correction is for "
-                                   "coalesced 16-B streams (our control reads 0.50x its known bytes); on this "
-                                   "kernel's 500-B-stride lane pattern a pure read of a known 524 MB reports 1.40x "
-                                   "(tools/fetch_calib.hip, profiles/r01c_fetch_calib.txt), the encrypt kernel "
-                                   "1.32x of its algorithmic reads: no over-fetch beyond the access pattern's own"}
+                    "calibration": "roofline.traffic = bytes_calibrated where the kernel's read pattern is "
+                                   "calibrated (FETCH_SIZE x the pattern's known/counted ratio + WRITE_SIZE), else "
+                                   "FETCH_SIZE x 2 + WRITE_SIZE (the guide's correction for coalesced 16-B streams, "
+                                   "whose 128-B requests are tallied at 64 B: our control reads 0.50x its known "
+                                   "bytes); bytes = FETCH_SIZE + WRITE_SIZE as counted. Pure reads of known bytes "
+                                   "(tools/fetch_calib.sh, profiles/r06_fetch_calib.txt): packed 560-B token rows "
+                                   "0.933x, the same tokens with each ciphertext on a line 0.684x, 500-B plaintext "
+                                   "rows in 64-B steps 1.408x"}
     return None
 
 

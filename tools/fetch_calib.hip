@@ -8,7 +8,7 @@
 // k_stream: the coalesced control — consecutive lanes read consecutive 16 B.
 // Both read the same 2^20 x 500 B = 524 288 000 bytes once; each writes 4 B
 // per lane.  Run each under `rocprofv3 --pmc FETCH_SIZE` and compare.
-//   hipcc --offload-arch=gfx950 -O3 -o build_tools/fetch_calib tools/fetch_calib.hip
+//   hipcc --offload-arch=gfx950 -O3 -o tools/_bin/fetch_calib tools/fetch_calib.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -40,6 +40,28 @@ __global__ __launch_bounds__(1024) void k_packets(const uint8_t *pt, uint32_t *o
     }
 }
 
+// k_rows: like k_decrypt's token reads — lane p reads row p (560 B = 35 16-B
+// units at a ROW-byte stride, first row at byte OFF), the IV first, then the
+// units in groups of 8 (the paired quads), a VALU delay between groups.
+// Known bytes: N x 560.  ROW 560 / OFF 0: packed c2 tokens; ROW 640 / OFF 112:
+// each token's ciphertext on a 128-B line.
+template <uint32_t ROW, uint32_t OFF>
+__global__ __launch_bounds__(768) void k_rows(const uint8_t *tok, uint32_t *out, int spin) {
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < N; p += gridDim.x * blockDim.x) {
+        const uint8_t *P = tok + OFF + (uint64_t)p * ROW;
+        u32x4 acc = ld16(P);
+        for (uint32_t g = 0; g < 34u; g += 8u) {
+            u32x4 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = g + 1u + k < 35u ? ld16(P + 16 * (g + 1u + k)) : acc;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc ^= v[k];
+            for (int k = 0; k < spin; ++k) acc.x = acc.x * 2654435761u + 1u;
+        }
+        out[p] = acc.x ^ acc.y ^ acc.z ^ acc.w;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_stream(const uint8_t *pt, uint32_t *out) {
     const uint64_t n16 = (uint64_t)N * L / 16;
     uint32_t acc = 0;
@@ -57,16 +79,21 @@ int main(int argc, char **argv) {
     const int ncu = prop.multiProcessorCount;
     uint8_t *pt;
     uint32_t *out;
-    CHECK(hipMalloc(&pt, (uint64_t)N * L + 64));
+    CHECK(hipMalloc(&pt, (uint64_t)N * 640 + 256));
     CHECK(hipMalloc(&out, 4ull * N));
-    CHECK(hipMemset(pt, 0x5a, (uint64_t)N * L + 64));
+    CHECK(hipMemset(pt, 0x5a, (uint64_t)N * 640 + 256));
     for (int r = 0; r < 3; ++r) {
         if (strcmp(which, "stream") == 0)
             hipLaunchKernelGGL(k_stream, dim3(ncu * 8), dim3(256), 0, 0, pt, out);
+        else if (strcmp(which, "rows560") == 0)
+            hipLaunchKernelGGL((k_rows<560, 0>), dim3(ncu), dim3(768), 0, 0, pt, out, 400);
+        else if (strcmp(which, "rows640") == 0)
+            hipLaunchKernelGGL((k_rows<640, 112>), dim3(ncu), dim3(768), 0, 0, pt, out, 400);
         else
             hipLaunchKernelGGL(k_packets, dim3(ncu), dim3(1024), 0, 0, pt, out, 200);
         CHECK(hipDeviceSynchronize());
     }
-    printf("%s: %llu bytes read per launch (algorithmic)\n", which, (unsigned long long)N * L);
+    printf("%s: %llu bytes read per launch (algorithmic)\n", which,
+           (unsigned long long)N * (strncmp(which, "rows", 4) == 0 ? 560u : L));
     return 0;
 }

@@ -230,16 +230,16 @@ def test_split_sector_grouped_stores_every_phase(rt, L, extra_stride, base_off, 
         assert t_h[i].tobytes() == oracle.encrypt(keys[kx[i]].tobytes(), iv_h[i].tobytes(), p_h[i].tobytes()), i
 
 
-@pytest.mark.parametrize("n_keys", [1, 65536])
-def test_split_sector_grouped_stores_packed_length_ordered(rt, n_keys):
+@pytest.mark.parametrize("n_keys,shift", [(1, 48), (65536, 48), (1, 7), (65536, 9)])
+def test_split_sector_grouped_stores_packed_length_ordered(rt, n_keys, shift):
     """The length-ordered packed path (c5's encrypt half) with sector-grouped
-    stores: tokens at prefix-sum offsets from a 16-B-misaligned first one, into a
+    stores: tokens at prefix-sum offsets (on and off the 16-B grid), into a
     sentinel-filled buffer; every token round-trips, a sample equals the oracle,
     and no byte outside the tokens is written."""
     import torch
     from reticulum_amd import _native, device
     n = _split_n(3)
-    rng = np.random.Generator(np.random.PCG64(4242 + n_keys))
+    rng = np.random.Generator(np.random.PCG64(4242 + n_keys + shift))
     keys = rng.integers(0, 256, (n_keys, 64), dtype=np.uint8)
     ks = rt.KeySet(keys if n_keys > 1 else keys[0].tobytes())
     kidx = torch.from_numpy(rng.integers(0, n_keys, n).astype(np.int32)).cuda() if n_keys > 1 else None
@@ -249,7 +249,7 @@ def test_split_sector_grouped_stores_packed_length_ordered(rt, n_keys):
     tl = (16 + 16 * (lens // 16 + 1) + 32).astype(np.int64)
     toff = np.zeros(n, np.int64)
     toff[1:] = np.cumsum(tl[:-1])
-    toff += 48
+    toff += shift            # 48: 16-B-aligned tokens; 7 / 9: tokens off the 16-B grid
     cu = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
     g = torch.Generator(device="cuda").manual_seed(99)
     buf = torch.randint(0, 256, (int(lens.astype(np.int64).sum()) + 1,), dtype=torch.uint8, device="cuda", generator=g)

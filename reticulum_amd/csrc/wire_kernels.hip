@@ -26,6 +26,13 @@
 #include "token_launch.h"
 #include "../../include/rnstok.h"
 
+// IFAC mask/unmask: payload stores grouped by 64-B sector, as k_encrypt_split's
+// ciphertext (round 6): node path, each build its own process, three runs each,
+// outbound 2.632 -> 2.615 ms, inbound 3.260 -> 3.223 ms (profiles/r06_clock_ab/ifac_sector_ab.txt)
+#ifndef RNSTOK_IFAC_ST_SECTOR
+#define RNSTOK_IFAC_ST_SECTOR 1
+#endif
+
 namespace rnstok {
 
 namespace {
@@ -751,6 +758,12 @@ __global__ __attribute__((amdgpu_waves_per_eu(4, 4))) __launch_bounds__(256) voi
         key_midstates(prkb, 32, phi, pho);
     }
     uint32_t t[8];
+    // RNSTOK_IFAC_ST_SECTOR: payload units are stored by 64-B sector in one
+    // burst (as k_encrypt_split's ciphertext): units of a sector the next
+    // chunk completes are held (up to 3: h0..h2 at hdst + 16 k)
+    u32x4 h0 = {0u, 0u, 0u, 0u}, h1 = h0, h2 = h0;
+    uint8_t *hdst = nullptr;
+    uint32_t nh = 0;
     for (uint32_t b = 0; 32u * b < total; ++b) {
         // message T_{b-1} (32 B, none for b = 0) || counter byte
         uint32_t w[16], h[8];
@@ -777,9 +790,36 @@ __global__ __attribute__((amdgpu_waves_per_eu(4, 4))) __launch_bounds__(256) voi
             const u32x4 m1 = {bswap(t[4]), bswap(t[5]), bswap(t[6]), bswap(t[7])};
             const uint8_t *src = MASK ? raw + (lo - n) : raw + lo;
             uint8_t *dst = MASK ? o + lo : o + (lo - n);
-            st16(dst, ld16(src) ^ m0);
-            st16(dst + 16, ld16(src + 16) ^ m1);
+            const u32x4 d0 = ld16(src) ^ m0, d1 = ld16(src + 16) ^ m1;
+            if (RNSTOK_IFAC_ST_SECTOR) {
+                // phases of d0 / d1 in their 64-B sector; held units precede d0
+                const uint32_t ph = ((uint32_t)(uintptr_t)dst >> 4) & 3u;
+                if (ph == 2u || ph == 3u) {            // d0 (and d1 at phase 3) closes the open sector
+                    if (nh > 0u) st16(hdst, h0);
+                    if (nh > 1u) st16(hdst + 16, h1);
+                    if (nh > 2u) st16(hdst + 32, h2);
+                    st16(dst, d0);
+                    if (ph == 2u) {
+                        st16(dst + 16, d1);
+                        nh = 0u;
+                    } else {
+                        h0 = d1; hdst = dst + 16; nh = 1u;
+                    }
+                } else {                              // phases 0/1: the sector closes with the next chunk
+                    if (nh == 0u) { h0 = d0; h1 = d1; hdst = dst; nh = 2u; }
+                    else { h1 = d0; h2 = d1; nh = 3u; }
+                }
+            } else {
+                st16(dst, d0);
+                st16(dst + 16, d1);
+            }
             continue;
+        }
+        if (RNSTOK_IFAC_ST_SECTOR && nh) {            // the tail's bytes follow: flush the held units
+            st16(hdst, h0);
+            if (nh > 1u) st16(hdst + 16, h1);
+            if (nh > 2u) st16(hdst + 32, h2);
+            nh = 0u;
         }
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
@@ -800,6 +840,11 @@ __global__ __attribute__((amdgpu_waves_per_eu(4, 4))) __launch_bounds__(256) voi
                 else if (pos >= 2u + n) o[pos - n] = raw[pos] ^ m;
             }
         }
+    }
+    if (RNSTOK_IFAC_ST_SECTOR && nh) {
+        st16(hdst, h0);
+        if (nh > 1u) st16(hdst + 16, h1);
+        if (nh > 2u) st16(hdst + 32, h2);
     }
 }
 

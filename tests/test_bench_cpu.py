@@ -165,3 +165,25 @@ def test_committed_n_gt_1_lines_carry_every_north_star_number():
             ph = sc["phases"][name]
             assert min(ph["scatter_ms"], ph["compute_ms"], ph["gather_ms"], ph["pipelined_ms"]) > 0
             assert ph["pipelined_equals_serial"] is True and ph["pipelined_chunks"] >= 1
+
+
+def test_ceiling_fracs_and_calibrated_traffic():
+    """Round 6: the bench line's ceiling fractions (canonical lane-ops over the
+    ISA slot floor at two wave64 instructions per slot) and the decrypt's
+    traffic from FETCH_SIZE scaled by its own read pattern's calibration."""
+    sys.path.insert(0, ROOT)
+    import bench
+    c = bench.ceiling_fracs("decrypt", 500, 1, 0.40)
+    ops = 64 * bench.ops_dec(500)
+    floor = bench.SLOTS_PER_WAVE_PACKET_500B["decrypt"]["floor"]
+    assert abs(c["ceiling_frac"] - ops / (floor * 128)) < 1e-12
+    assert 0.45 < c["ceiling_frac"] < 0.52 and 0.6 < c["ceiling_frac_valu_only"] < 0.72
+    assert abs(c["frac_over_ceiling"] - 0.40 / c["ceiling_frac"]) < 1e-12
+    assert bench.ceiling_fracs("decrypt", 383, 1, 0.4)["ceiling_frac"] is None        # c2 shape only
+    t = bench.traffic_from_profiles("decrypt", 1 << 20, 500, 1, "rows")
+    k, _ = bench.FETCH_CALIBRATION[("decrypt", "rows")]
+    path, d = bench._newest_pmc("decrypt", 1 << 20, 500, 1)
+    m = d["decrypt"]
+    assert abs(t["bytes_calibrated"] - (k * m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024) < 1.0
+    assert t["bytes_calibrated"] < t["bytes_with_x2_fetch_correction"]
+    assert bench.traffic_from_profiles("encrypt", 1 << 20, 500, 1, "rows")["bytes_calibrated"] is None

@@ -435,7 +435,10 @@ __global__ RT_OCC __launch_bounds__(PERKEY ? WG_PERKEY_ENC : WG_ENC) void k_encr
 // keys (PERKEY: each AES lane loads its packet's round keys, each hashing lane
 // its ipad/opad midstates, from the 544-B key records; 128 VGPRs, 2 spilled
 // on rows).
-constexpr uint32_t SPLIT_AES_WAVES = 8, SPLIT_THREADS = 1024;
+#ifndef RNSTOK_SPLIT_AES_WAVES       // AES waves (= hashing waves) per workgroup (experiment knob)
+#define RNSTOK_SPLIT_AES_WAVES 8
+#endif
+constexpr uint32_t SPLIT_AES_WAVES = RNSTOK_SPLIT_AES_WAVES, SPLIT_THREADS = 128u * RNSTOK_SPLIT_AES_WAVES;
 constexpr uint32_t SPLIT_RING = LDS_ENC_BYTES;                    // 8 x 4 KiB
 constexpr uint32_t LDS_ENC_SPLIT_BYTES = SPLIT_RING + SPLIT_AES_WAVES * 4096u;
 static_assert(LDS_ENC_SPLIT_BYTES <= 160u * 1024u, "LDS");

@@ -38,15 +38,6 @@ namespace rnstok {
 #ifndef RNSTOK_DEC_PAIR              // decrypt, one key, token quads loaded in pairs: fetch -21 %, time -1.6 %
 #define RNSTOK_DEC_PAIR 1
 #endif
-#ifndef RNSTOK_DEC_ST_SECTOR         // decrypt: plaintext stores grouped by 64-B sector (experiment)
-#define RNSTOK_DEC_ST_SECTOR 0
-#endif
-#ifndef RNSTOK_DEC_ST_SECTOR_PERKEY
-#define RNSTOK_DEC_ST_SECTOR_PERKEY 0
-#endif
-#ifndef RNSTOK_DEC_SHIFT_WAVES       // decrypt: per-wave full-rate address experiment (bit mask of wave slots)
-#define RNSTOK_DEC_SHIFT_WAVES 0
-#endif
 // Split encrypt, packed rows: the ciphertext units of a 64-B sector that a quad
 // shares with the next quad are held and stored with the next quad's, so every
 // sector leaves in one burst of stores (fabric write requests 18.3 M -> 12.8 M
@@ -1144,12 +1135,6 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
             // L2 through and the line is fetched again: 2.7x read traffic)
             constexpr bool PAIR = RNSTOK_DEC_PAIR && !ILV && !PERKEY && WG <= 768;   // (1024: 11 -> 38 VGPRs spilled)
             u32x4 nx[4];
-            // RNSTOK_DEC_ST_SECTOR (experiment): plaintext stores grouped by 64-B
-            // sector, as k_encrypt_split's ciphertext stores (dsg: the sector
-            // phase of the lane's output, in units; 0 = every quad on a sector)
-            constexpr bool DSECT = !ILV && (PERKEY ? RNSTOK_DEC_ST_SECTOR_PERKEY : RNSTOK_DEC_ST_SECTOR);
-            const uint32_t dsg = DSECT ? ((uint32_t)(uintptr_t)O >> 4) & 3u : 0u;
-            u32x4 hp1 = z, hp2 = z, hp3 = z;
 #pragma nounroll
             for (uint32_t q = 0; q <= nq; ++q) {
                 const uint32_t nbk = q < nq ? 4u : tb;
@@ -1171,42 +1156,16 @@ __global__ RT_OCC __launch_bounds__(WG) void k_decrypt(DecArgs a) {
                 }
                 S.start(h);
                 sha_units(S.w, prev, c[0], c[1], c[2]);
-#if RNSTOK_DEC_SHIFT_WAVES
-                // experiment (round 6): the waves in the slots of RNSTOK_DEC_SHIFT_WAVES
-                // (bit k: the (k+1)-th wave of each SIMD) build T-table addresses from
-                // full-rate shift + bitop3 instead of v_perm
-                if (!PERKEY && !ILV && ((RNSTOK_DEC_SHIFT_WAVES >> (threadIdx.x >> 8)) & 1))
-                    dec_quad<NR, true, true>(pp, c, prev, K.rk, LN, S);
-                else
-#endif
                 dec_quad<NR, true>(pp, c, prev, K.rk, LN, S);
 #pragma unroll
                 for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(S.v[k]));   // see k_encrypt
                 const bool keep = nbk >= 3u;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) h[k] += keep ? S.v[k] : 0u;
-                if (DSECT) {
-                    // the held units of the previous quad's last sector, then this
-                    // quad's units up to its first sector boundary (all at the tail)
-                    if (q != 0u) {
-                        if (dsg == 3u) st16(D - 3 * US, hp1);
-                        if (dsg >= 2u) st16(D - 2 * US, hp2);
-                        if (dsg >= 1u) st16(D - US, hp3);
-                    }
-                    const uint32_t now = q == nq ? nbk : (4u - dsg < nbk ? 4u - dsg : nbk);
-                    st16(D, pp[0]);
-                    if (now > 1u) st16(D + US, pp[1]);
-                    if (now > 2u) st16(D + 2 * US, pp[2]);
-                    if (now > 3u) st16(D + 3 * US, pp[3]);
-                    hp1 = pp[1];
-                    hp2 = pp[2];
-                    hp3 = pp[3];
-                } else {
-                    st16(D, pp[0]);
-                    if (nbk > 1u) st16(D + US, pp[1]);
-                    if (nbk > 2u) st16(D + 2 * US, pp[2]);
-                    if (nbk > 3u) st16(D + 3 * US, pp[3]);
-                }
+                st16(D, pp[0]);
+                if (nbk > 1u) st16(D + US, pp[1]);
+                if (nbk > 2u) st16(D + 2 * US, pp[2]);
+                if (nbk > 3u) st16(D + 3 * US, pp[3]);
                 prev = c[3];
                 C += 4 * US; D += 4 * US;
             }

@@ -1394,7 +1394,7 @@ def per_call_rate(threads=16, calls=200, L=383, seconds_cap=20.0):
     Token call per packet, from many interface and application threads):
     ``threads`` threads, each with its own link key, alternately encrypting a
     ``L``-byte packet and decrypting the token through ``Token`` (one GPU
-    round trip per call; the host entry points' four staging lanes let four
+    round trip per call; the host entry points' eight staging lanes let eight
     run at once), and the same from one thread.  Calls/s over all threads."""
     import threading
     import reticulum_amd as rt

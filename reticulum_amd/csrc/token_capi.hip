@@ -37,7 +37,15 @@ struct Stager {
     uint64_t stage_cap = 0;
     bool stage_busy = false;       // a copy from h_stage may still be queued on `stream`
 };
-static constexpr int N_STAGERS = 4;
+// 8 lanes (round 6): one Token call per packet from 16 threads, 44 600 ->
+// 73 000 calls/s against 4 lanes (two runs each, profiles/r06_percall_lanes.txt;
+// one thread unchanged at 19 000); streams beyond the box's four hardware
+// queues still overlap the host-side waits of concurrent calls.  Pinned
+// staging grows on demand, at most 8 MiB per lane.
+#ifndef RNSTOK_N_STAGERS
+#define RNSTOK_N_STAGERS 8
+#endif
+static constexpr int N_STAGERS = RNSTOK_N_STAGERS;
 
 // Chunk counters for the token kernels' dynamic packet loop (ragged uniform
 // batches): one 64-B slot per launch.  A slot is handed out again only after

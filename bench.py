@@ -1389,7 +1389,7 @@ def shard_rate(dev, n_cu, steps=10, L=16384, per_cu=128):
     return res
 
 
-def per_call_rate(threads=16, calls=200, L=383, seconds_cap=20.0):
+def per_call_rate(threads=16, calls=1000, L=383, seconds_cap=20.0):
     """The reference's call pattern (RNS/Link.py:1161-1182: one synchronous
     Token call per packet, from many interface and application threads):
     ``threads`` threads, each with its own link key, alternately encrypting a

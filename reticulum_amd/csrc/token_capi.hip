@@ -235,6 +235,19 @@ static hipError_t copy_d2h(void *dst, const void *src, uint64_t bytes, hipStream
 static int ensure_work(Stager &g, uint64_t bytes);
 static uint8_t *stage(Stager &g, uint64_t bytes);
 
+// One packet per call (Token.encrypt / Token.decrypt): the token kernel reads
+// its inputs from the lane's mapped pinned staging buffer and writes its
+// outputs there, instead of a copy kernel in, the token kernel, and a store
+// kernel out (the runtime's H2D of a small pinned buffer is itself a blit
+// kernel, 2.4 us, and the store kernel 3.6 us, each plus its dispatch).  383-B
+// packets, one thread: Token.encrypt 57.8 -> 50.1 us, Token.decrypt 45.5 ->
+// 38.6 us, 19 100 -> 21 800 calls/s (three runs each,
+// profiles/r06_host_direct_ab.txt).  Batches keep the copies (their kernels
+// would read every packet across PCIe; not measured).
+#ifndef RNSTOK_HOST_DIRECT
+#define RNSTOK_HOST_DIRECT 1
+#endif
+
 // A key set whose records are allocated and built on stream s.  `build`
 // enqueues the kernel(s) that write k->d_rec.
 template <class Build>
@@ -721,6 +734,7 @@ int rt_encrypt_host(const rt_keyset *k, const uint8_t *pt, const uint64_t *pt_of
     hipStream_t s = g.stream;
     const bool gaps = tok_sum != tok_ext;   // gaps between tokens: keep the caller's bytes there
     uint8_t *h = stage(g, total);
+    const bool direct = RNSTOK_HOST_DIRECT && h && n == 1;
     if (h) {
         if (pt_ext) memcpy(h + o_pt, pt, pt_ext);
         memcpy(h + o_iv, iv, 16ull * n);
@@ -730,7 +744,7 @@ int rt_encrypt_host(const rt_keyset *k, const uint8_t *pt, const uint64_t *pt_of
         if (key_idx) memcpy(h + o_ki, key_idx, 4ull * n);
         if (gaps) memcpy(h + o_tok, tok, tok_ext);
         g.stage_busy = true;
-        RT_HIP(hipMemcpyAsync(w, h, gaps ? total : o_tok, hipMemcpyHostToDevice, s), "H2D stage");
+        if (!direct) RT_HIP(hipMemcpyAsync(w, h, gaps ? total : o_tok, hipMemcpyHostToDevice, s), "H2D stage");
     } else {
         if (pt_ext) RT_HIP(hipMemcpyAsync(w + o_pt, pt, pt_ext, hipMemcpyHostToDevice, s), "H2D pt");
         if (gaps) RT_HIP(hipMemcpyAsync(w + o_tok, tok, tok_ext, hipMemcpyHostToDevice, s), "H2D tok");
@@ -740,6 +754,7 @@ int rt_encrypt_host(const rt_keyset *k, const uint8_t *pt, const uint64_t *pt_of
         RT_HIP(hipMemcpyAsync(w + o_to, tok_off, 8ull * n, hipMemcpyHostToDevice, s), "H2D tok_off");
         if (key_idx) RT_HIP(hipMemcpyAsync(w + o_ki, key_idx, 4ull * n, hipMemcpyHostToDevice, s), "H2D key_idx");
     }
+    if (direct) w = g.h_stage_dev;
     EncArgs a{};
     a.pt = w + o_pt; a.pt_off = (const uint64_t *)(w + o_po); a.pt_len = (const uint32_t *)(w + o_pl);
     a.key_idx = key_idx ? (const uint32_t *)(w + o_ki) : nullptr; a.iv = w + o_iv;
@@ -749,7 +764,7 @@ int rt_encrypt_host(const rt_keyset *k, const uint8_t *pt, const uint64_t *pt_of
         a.tok += tok_off[0]; a.tok_off = nullptr;
     }
     if ((rc = enc_common(k, a, s))) return rc;
-    RT_HIP(h ? launch_store_host(g.h_stage_dev + o_tok, w + o_tok, tok_ext, s) : copy_d2h(tok, w + o_tok, tok_ext, s, k->ctx->device),
+    if (!direct) RT_HIP(h ? launch_store_host(g.h_stage_dev + o_tok, w + o_tok, tok_ext, s) : copy_d2h(tok, w + o_tok, tok_ext, s, k->ctx->device),
            "D2H tok");
     RT_HIP(hipStreamSynchronize(s), "stream sync");
     g.stage_busy = false;
@@ -788,6 +803,7 @@ int rt_decrypt_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_
     hipStream_t s = g.stream;
     const bool gaps = pt_ext && pt_sum != pt_ext;   // gaps between plaintexts: keep the caller's bytes there
     uint8_t *h = stage(g, total);
+    const bool direct = RNSTOK_HOST_DIRECT && h && n == 1;
     if (h) {
         if (tok_ext) memcpy(h + o_tok, tok, tok_ext);
         memcpy(h + o_to, tok_off, 8ull * n);
@@ -796,7 +812,7 @@ int rt_decrypt_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_
         if (key_idx) memcpy(h + o_ki, key_idx, 4ull * n);
         if (gaps) memcpy(h + o_pt, pt, pt_ext);
         g.stage_busy = true;
-        RT_HIP(hipMemcpyAsync(w, h, gaps ? o_ol : o_pt, hipMemcpyHostToDevice, s), "H2D stage");
+        if (!direct) RT_HIP(hipMemcpyAsync(w, h, gaps ? o_ol : o_pt, hipMemcpyHostToDevice, s), "H2D stage");
     } else {
         if (tok_ext) RT_HIP(hipMemcpyAsync(w + o_tok, tok, tok_ext, hipMemcpyHostToDevice, s), "H2D tok");
         if (gaps) RT_HIP(hipMemcpyAsync(w + o_pt, pt, pt_ext, hipMemcpyHostToDevice, s), "H2D pt");
@@ -805,6 +821,7 @@ int rt_decrypt_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_
         RT_HIP(hipMemcpyAsync(w + o_po, pt_off, 8ull * n, hipMemcpyHostToDevice, s), "H2D pt_off");
         if (key_idx) RT_HIP(hipMemcpyAsync(w + o_ki, key_idx, 4ull * n, hipMemcpyHostToDevice, s), "H2D key_idx");
     }
+    if (direct) w = g.h_stage_dev;
     DecArgs a{};
     a.tok = w + o_tok; a.tok_off = (const uint64_t *)(w + o_to); a.tok_len = (const uint32_t *)(w + o_tl);
     a.key_idx = key_idx ? (const uint32_t *)(w + o_ki) : nullptr; a.pt = w + o_pt;
@@ -816,7 +833,7 @@ int rt_decrypt_host(const rt_keyset *k, const uint8_t *tok, const uint64_t *tok_
     }
     if ((rc = dec_common(k, a, s))) return rc;
     if (h) {
-        RT_HIP(launch_store_host(g.h_stage_dev + o_pt, w + o_pt, total - o_pt, s), "D2H stage");
+        if (!direct) RT_HIP(launch_store_host(g.h_stage_dev + o_pt, w + o_pt, total - o_pt, s), "D2H stage");
         RT_HIP(hipStreamSynchronize(s), "stream sync");
         g.stage_busy = false;
         if (pt_ext) memcpy(pt, h + o_pt, pt_ext);

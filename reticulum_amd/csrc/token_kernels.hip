@@ -886,6 +886,16 @@ constexpr uint32_t L4_RING = LDS_ENC_BYTES;                              // afte
 // fused kernel's excess over its AES side alone (0.91 ms; hashing side alone
 // 0.73) is SIMD contention, not barrier jitter.
 constexpr uint32_t L4_SLOTS = 2u;
+// Waves none of whose lanes holds a token of the batch skip the rounds and
+// only meet the barriers.  In a launch of a few tokens (one Token call) their
+// chains on garbage took issue slots from the live AES and hashing chains
+// that share their SIMDs.
+#ifndef RNSTOK_L4_SKIP_IDLE
+#define RNSTOK_L4_SKIP_IDLE 1
+#endif
+#ifndef RNSTOK_L4_HASH_FIRST
+#define RNSTOK_L4_HASH_FIRST 1
+#endif
 constexpr uint32_t LDS_ENC_LONG4_BYTES = L4_RING + L4_SLOTS * L4_TOK * 64u;   // + 2 slots x 128 tokens x 64 B
 
 // DPP quad_perm: lane j of each group of four reads lane (j + K) & 3.
@@ -951,10 +961,15 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
     fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);
     const Lanes LN(threadIdx.x & 31u);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    const bool aes = wave < L4_AES_WAVES;
+    // RNSTOK_L4_HASH_FIRST: the hashing waves are waves 0-1 (SIMDs 0-1) and
+    // the first tokens' AES wave is wave 2, so a launch of a few tokens runs
+    // its AES and hashing chains on different SIMDs (else waves 0 and 8 shared
+    // SIMD 0); a full workgroup puts the same roles on each SIMD either way.
+    const uint32_t hw = RNSTOK_L4_HASH_FIRST ? (wave < L4_HASH_WAVES ? L4_AES_WAVES + wave : wave - L4_HASH_WAVES) : wave;
+    const bool aes = hw < L4_AES_WAVES;
     const uint32_t col = threadIdx.x & 3u;
     const bool hash_lane = aes || lane < L4_HASH_TOK;
-    const uint32_t slot = aes ? threadIdx.x >> 2 : (wave - L4_AES_WAVES) * L4_HASH_TOK + (hash_lane ? lane : 0u);
+    const uint32_t slot = aes ? (64u * hw + lane) >> 2 : (hw - L4_AES_WAVES) * L4_HASH_TOK + (hash_lane ? lane : 0u);
     const uint32_t L = a.uni_len, nfull = L >> 4, nq = nfull >> 2, tb = (nfull & 3u) + 1u, rem = L & 15u;
     uint32_t rk[NR + 1];
 #pragma unroll
@@ -966,6 +981,7 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
         const uint32_t p = valid ? (a.order ? a.order[t] : t) : 0u;
         const uint8_t *P = a.pt + (valid ? in_off(a.pt_off, a.pt_stride, p) : 0);
         uint8_t *O = a.tok + (valid ? in_off(a.tok_off, a.tok_stride, p) : 0);
+        const bool live = !RNSTOK_L4_SKIP_IDLE || __ballot(valid) != 0ull;     // wave-uniform
         if (aes) {
             // this lane's column of the plaintext blocks of quad k (the tail quad: tb blocks, the last padded)
             auto load_quad = [&](uint32_t k, uint32_t x[4]) {
@@ -983,15 +999,17 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
             for (uint32_t k = 0; k <= nq; ++k) {
                 const uint32_t x[4] = {xn[0], xn[1], xn[2], xn[3]};
                 if (k < nq) load_quad(k + 1u, xn);        // the next quad is requested before this quad's rounds
-                uint32_t cq[4];
+                uint32_t cq[4] = {0u, 0u, 0u, 0u};
+                if (live) {
 #pragma unroll
-                for (int b = 0; b < 4; ++b) {
+                    for (int b = 0; b < 4; ++b) {
 #ifndef RNSTOK_L4_PROBE_SHA_ONLY        // timing probe: no AES (wrong tokens)
-                    cq[b] = enc_block4<NR>(x[b] ^ prev, rk, LN);
+                        cq[b] = enc_block4<NR>(x[b] ^ prev, rk, LN);
 #else
-                    cq[b] = x[b] ^ prev;
+                        cq[b] = x[b] ^ prev;
 #endif
-                    prev = cq[b];
+                        prev = cq[b];
+                    }
                 }
                 const uint32_t nst = k < nq ? 4u : tb;
                 uint8_t *Ck = O + 16 + 64ull * k + 4u * col;
@@ -1018,9 +1036,11 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
                 const u32x4 c0 = r[0], c1 = r[1], c2 = r[2], c3 = r[3];
                 if (q < nq) {
 #ifndef RNSTOK_L4_PROBE_AES_ONLY        // timing probe: no HMAC (wrong tags)
-                    uint32_t w[16];
-                    sha_units(w, prev, c0, c1, c2);
-                    sha256_compress(h, w);
+                    if (live) {
+                        uint32_t w[16];
+                        sha_units(w, prev, c0, c1, c2);
+                        sha256_compress(h, w);
+                    }
 #endif
                     prev = c3;
                 } else if (valid) {

@@ -1262,6 +1262,17 @@ constexpr uint32_t DL2_RING = 0x14000;                       // 2 slots x 16 qua
 constexpr uint32_t DL2_SLOT = 16u * DL2_TOK * 16u;           // 32 KiB
 constexpr uint32_t DL2_FLAGS = DL2_RING + 2u * DL2_SLOT;     // ready[2], done[2] (u32)
 constexpr uint32_t LDS_DL2_BYTES = DL2_FLAGS + 64u;
+// The producers also schedule the final padded block, so the chain runs it
+// from the ring like the others (its own schedule inline took a third more
+// instructions per round).
+#ifndef RNSTOK_DL2_FINAL
+#define RNSTOK_DL2_FINAL 1
+#endif
+constexpr bool DL2_FINAL = RNSTOK_DL2_FINAL;
+#ifndef RNSTOK_DL2_SKIP_IDLE
+#define RNSTOK_DL2_SKIP_IDLE 1
+#endif
+constexpr bool DL2_SKIP_IDLE = RNSTOK_DL2_SKIP_IDLE;
 
 __device__ void fill_tables_dl2(uint32_t *tab, const uint8_t *inv) {
     const uint32_t lane = threadIdx.x & 31u;
@@ -1381,18 +1392,37 @@ __global__ __launch_bounds__(DL2_THREADS) void k_decrypt_long2(DecArgs a) {
         const uint32_t ntok = a.n - base < DL2_TOK ? a.n - base : DL2_TOK;
         const uint32_t slot_tok = pair * 64u + lane;            // this lane's column of the ring
         uint32_t diff = 1;
-        if (producer) {
+        // DL2_SKIP_IDLE: a batch of at most 64 tokens leaves chain pair 1
+        // without a token; it skips its chains, and only the AES waves on
+        // SIMDs 1 and 3 take quads, so the live chain waves (0 on SIMD 0, 2 on
+        // SIMD 2) share their SIMDs with nothing (one Token call)
+        const bool idle = DL2_SKIP_IDLE && ((consumer || producer) ? pair * 64u >= ntok : (ntok <= 64u && !(wave & 1u)));
+        if (idle) {
+        } else if (producer) {
             // tokens past the batch hash a copy of its last token (results unused)
             const uint32_t t = base + (slot_tok < ntok ? slot_tok : ntok - 1u);
             const uint8_t *Kt = a.tok + in_off(a.tok_off, a.tok_stride, a.order ? a.order[t] : t);
-            u32x4 b0 = ld16(Kt), b1 = ld16(Kt + 16), b2 = ld16(Kt + 32), b3 = ld16(Kt + 48);
-            for (uint32_t i = 0; i < full; ++i) {
+            // the final padded block (the last fu units of iv || ct) too, with DL2_FINAL
+            const uint32_t fu = (M - 64u * full) >> 4, nblk = full + (DL2_FINAL ? 1u : 0u);
+            const u32x4 z = {0u, 0u, 0u, 0u};
+            auto load_block = [&](uint32_t i, u32x4 &c0, u32x4 &c1, u32x4 &c2, u32x4 &c3) {
+                const uint8_t *B = Kt + 64ull * i;
+                const uint32_t nu = i < full ? 4u : fu;         // (the final block's units stop at the tag)
+                c0 = nu > 0u ? ld16(B) : z; c1 = nu > 1u ? ld16(B + 16) : z;
+                c2 = nu > 2u ? ld16(B + 32) : z; c3 = nu > 3u ? ld16(B + 48) : z;
+            };
+            u32x4 b0, b1, b2, b3;
+            load_block(0u, b0, b1, b2, b3);
+            for (uint32_t i = 0; i < nblk; ++i) {
                 uint32_t w[16];
                 sha_units(w, b0, b1, b2, b3);
-                if (i + 1 < full) {                             // next block requested before this schedule
-                    const uint8_t *B = Kt + 64ull * (i + 1);
-                    b0 = ld16(B); b1 = ld16(B + 16); b2 = ld16(B + 32); b3 = ld16(B + 48);
+                if (DL2_FINAL && i == full) {
+                    uint32_t fin[16];
+                    sha_final_block(fin, w, fu, (uint64_t)(64u + M) * 8u);
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) w[k] = fin[k];
                 }
+                if (i + 1 < nblk) load_block(i + 1u, b0, b1, b2, b3);     // next block requested before this schedule
                 if (i >= 2u) dl2_wait(done_f, i - 1u);           // the consumer is done with slot i & 1
                 lds_quad_t *ring = (lds_quad_t *)(uintptr_t)(DL2_RING + (i & 1u) * DL2_SLOT) + slot_tok;
                 constexpr uint32_t Kc[64] = {
@@ -1432,7 +1462,7 @@ __global__ __launch_bounds__(DL2_THREADS) void k_decrypt_long2(DecArgs a) {
                                                a.order ? a.order[valid ? t : base] : (valid ? t : base));
             uint32_t h[8], opad[8];
             load_uniform8(h, a.rec + REC_IPAD);
-            for (uint32_t i = 0; i < full; ++i) {
+            for (uint32_t i = 0; i < full + (DL2_FINAL ? 1u : 0u); ++i) {
                 dl2_wait(ready_f, i + 1u);
                 const lds_quad_t *ring = (const lds_quad_t *)(uintptr_t)(DL2_RING + (i & 1u) * DL2_SLOT) + slot_tok;
                 uint32_t v[8];
@@ -1457,11 +1487,13 @@ __global__ __launch_bounds__(DL2_THREADS) void k_decrypt_long2(DecArgs a) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) h[k] += v[k];
             }
-            const uint32_t fu = (M - 64u * full) >> 4;
-            const u32x4 z = {0u, 0u, 0u, 0u};
-            const uint8_t *R = Kt + 64ull * full;
-            sha_final_units(h, fu, fu > 0 ? ld16(R) : z, fu > 1 ? ld16(R + 16) : z, fu > 2 ? ld16(R + 32) : z,
-                            (uint64_t)(64u + M) * 8u);
+            if (!DL2_FINAL) {
+                const uint32_t fu = (M - 64u * full) >> 4;
+                const u32x4 z = {0u, 0u, 0u, 0u};
+                const uint8_t *R = Kt + 64ull * full;
+                sha_final_units(h, fu, fu > 0 ? ld16(R) : z, fu > 1 ? ld16(R + 16) : z, fu > 2 ? ld16(R + 32) : z,
+                                (uint64_t)(64u + M) * 8u);
+            }
             load_uniform8(opad, a.rec + REC_OPAD);
             uint32_t tag[8];
             hmac_outer(tag, h, opad);

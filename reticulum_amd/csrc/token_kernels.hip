@@ -958,7 +958,6 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
     typedef __attribute__((address_space(3))) const u32x4 lds_q;
     LaunchClock clk;
     clk.start(a.clk);
-    fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);
     const Lanes LN(threadIdx.x & 31u);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     // RNSTOK_L4_HASH_FIRST: the hashing waves are waves 0-1 (SIMDs 0-1) and
@@ -982,20 +981,31 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
         const uint8_t *P = a.pt + (valid ? in_off(a.pt_off, a.pt_stride, p) : 0);
         uint8_t *O = a.tok + (valid ? in_off(a.tok_off, a.tok_stride, p) : 0);
         const bool live = !RNSTOK_L4_SKIP_IDLE || __ballot(valid) != 0ull;     // wave-uniform
-        if (aes) {
-            // this lane's column of the plaintext blocks of quad k (the tail quad: tb blocks, the last padded)
-            auto load_quad = [&](uint32_t k, uint32_t x[4]) {
+        // this lane's column of the plaintext blocks of quad k (the tail quad: tb blocks, the last padded)
+        auto load_quad = [&](uint32_t k, uint32_t x[4]) {
 #pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const uint8_t *B = P + 16ull * (4u * k + (uint32_t)b);
-                    x[b] = !valid ? 0u
-                                  : ((k < nq || (uint32_t)b + 1u < tb) ? ld32u(B + 4u * col)
-                                                                        : ((uint32_t)b + 1u == tb ? pad_col(B, rem, col) : 0u));
-                }
-            };
-            uint32_t prev = valid ? ld32u(a.iv + 16ull * p + 4u * col) : 0u, xn[4];
-            if (valid) st32u(O + 4u * col, prev);
+            for (int b = 0; b < 4; ++b) {
+                const uint8_t *B = P + 16ull * (4u * k + (uint32_t)b);
+                x[b] = !valid ? 0u
+                              : ((k < nq || (uint32_t)b + 1u < tb) ? ld32u(B + 4u * col)
+                                                                    : ((uint32_t)b + 1u == tb ? pad_col(B, rem, col) : 0u));
+            }
+        };
+        // The batch's IV (each AES lane's column, each hashing lane's whole
+        // unit) and first quad are requested before the first batch's table
+        // fill: for a Token call they sit in the pinned staging buffer, and
+        // the fill hides that PCIe round trip.
+        uint32_t prev = 0u, xn[4] = {0u, 0u, 0u, 0u};
+        u32x4 hiv = {0u, 0u, 0u, 0u};
+        if (aes) {
+            prev = valid ? ld32u(a.iv + 16ull * p + 4u * col) : 0u;
             load_quad(0u, xn);
+        } else if (valid) {
+            hiv = ld16(a.iv + 16ull * p);
+        }
+        if (base == blockIdx.x * L4_TOK) fill_tables<false>(tab_u32, a.sbox, a.sbox + 256);   // (workgroup-uniform)
+        if (aes) {
+            if (valid) st32u(O + 4u * col, prev);
             for (uint32_t k = 0; k <= nq; ++k) {
                 const uint32_t x[4] = {xn[0], xn[1], xn[2], xn[3]};
                 if (k < nq) load_quad(k + 1u, xn);        // the next quad is requested before this quad's rounds
@@ -1028,7 +1038,7 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
             uint32_t h[8], opad[8];
             load_uniform8(h, a.rec + REC_IPAD);
             load_uniform8(opad, a.rec + REC_OPAD);
-            u32x4 prev = valid ? ld16(a.iv + 16ull * p) : u32x4{0u, 0u, 0u, 0u};
+            u32x4 prev = hiv;
             const uint64_t bits = (uint64_t)(64u + 16u + 16u * (nfull + 1u)) * 8u;
             __syncthreads();         // step 0: nothing to hash yet
             for (uint32_t q = 0; q <= nq; ++q) {
@@ -1261,7 +1271,8 @@ constexpr uint32_t DL2_INVS = 0x10000;                       // 256 rows x 64 B:
 constexpr uint32_t DL2_RING = 0x14000;                       // 2 slots x 16 quads x 128 tokens x 16 B
 constexpr uint32_t DL2_SLOT = 16u * DL2_TOK * 16u;           // 32 KiB
 constexpr uint32_t DL2_FLAGS = DL2_RING + 2u * DL2_SLOT;     // ready[2], done[2] (u32)
-constexpr uint32_t LDS_DL2_BYTES = DL2_FLAGS + 64u;
+constexpr uint32_t DL2_PADN = DL2_FLAGS + 64u;                // per token of the batch: its last plaintext byte
+constexpr uint32_t LDS_DL2_BYTES = DL2_PADN + 4u * DL2_TOK;
 // The producers also schedule the final padded block, so the chain runs it
 // from the ring like the others (its own schedule inline took a third more
 // instructions per round).
@@ -1462,6 +1473,9 @@ __global__ __launch_bounds__(DL2_THREADS) void k_decrypt_long2(DecArgs a) {
                                                a.order ? a.order[valid ? t : base] : (valid ? t : base));
             uint32_t h[8], opad[8];
             load_uniform8(h, a.rec + REC_IPAD);
+            // the tag, requested before the chain (a Token call's token sits in
+            // pinned host memory: one PCIe round trip less at the end)
+            const u32x4 r0 = ld16(Kt + M), r1 = ld16(Kt + M + 16);
             for (uint32_t i = 0; i < full + (DL2_FINAL ? 1u : 0u); ++i) {
                 dl2_wait(ready_f, i + 1u);
                 const lds_quad_t *ring = (const lds_quad_t *)(uintptr_t)(DL2_RING + (i & 1u) * DL2_SLOT) + slot_tok;
@@ -1497,7 +1511,6 @@ __global__ __launch_bounds__(DL2_THREADS) void k_decrypt_long2(DecArgs a) {
             load_uniform8(opad, a.rec + REC_OPAD);
             uint32_t tag[8];
             hmac_outer(tag, h, opad);
-            const u32x4 r0 = ld16(Kt + M), r1 = ld16(Kt + M + 16);
             diff = (r0.x ^ bswap(tag[0])) | (r0.y ^ bswap(tag[1])) | (r0.z ^ bswap(tag[2])) |
                    (r0.w ^ bswap(tag[3])) | (r1.x ^ bswap(tag[4])) | (r1.y ^ bswap(tag[5])) |
                    (r1.z ^ bswap(tag[6])) | (r1.w ^ bswap(tag[7]));
@@ -1539,6 +1552,10 @@ __global__ __launch_bounds__(DL2_THREADS) void k_decrypt_long2(DecArgs a) {
                     if (nbk > 1) st16(D + 16, pp[1]);
                     if (nbk > 2) st16(D + 32, pp[2]);
                     if (nbk > 3) st16(D + 48, pp[3]);
+                    if (q + 1u == nquads) {             // PKCS7.unpad's n = data[-1], for the chain wave
+                        const u32x4 last = nbk == 1u ? pp[0] : (nbk == 2u ? pp[1] : (nbk == 3u ? pp[2] : pp[3]));
+                        *(lds_word_t *)(uintptr_t)(DL2_PADN + 4u * (t - base)) = last.w >> 24;
+                    }
                 }
             }
         }
@@ -1548,7 +1565,7 @@ __global__ __launch_bounds__(DL2_THREADS) void k_decrypt_long2(DecArgs a) {
             if (slot_tok < ntok) {
                 const uint32_t p = a.order ? a.order[t] : t;
                 uint8_t *O = a.pt + in_off(a.pt_off, a.pt_stride, p);
-                const uint32_t padn = O[16u * nb - 1u];       // PKCS7.unpad: n = data[-1]
+                const uint32_t padn = *(lds_word_t *)(uintptr_t)(DL2_PADN + 4u * slot_tok);   // PKCS7.unpad: n = data[-1]
                 const int32_t st = diff ? 2 : (padn > 16u ? 4 : 0);
                 const uint32_t outlen = st == 0 ? 16u * nb - padn : (st == 4 ? padn : 0u);
                 if (st != 0) {

@@ -51,6 +51,21 @@ def main():
             res[name] = {"us": round(s["wg_span_ms"] * 1e3, 2), "kcycles": round(s["cycles_per_launch"] / 1e3, 2),
                          "clock_ghz": round(s["clock_ghz"], 3)}
         res["round_trip_ok"] = bool(int(st[0]) == 0 and torch.equal(back[0, :L], pt[0]))
+        # the same kernels behind Token (rt_*_host, n = 1: inputs and outputs in the mapped pinned staging buffer)
+        tk, msg = rt.Token(os.urandom(64)), os.urandom(L)
+        for name, f in (("token_encrypt", lambda: tk.encrypt(msg)), ("token_decrypt", None)):
+            if f is None:
+                t0 = tk.encrypt(msg)
+                f = lambda: tk.decrypt(t0)      # noqa: E731
+            for _ in range(30):
+                f()
+            with device.LaunchClock(dev) as lc:
+                for _ in range(args.calls):
+                    f()
+            s = lc.summary().get(name.split("_")[1])
+            if s is not None:
+                res[name] = {"us": round(s["wg_span_ms"] * 1e3, 2), "kcycles": round(s["cycles_per_launch"] / 1e3, 2),
+                             "clock_ghz": round(s["clock_ghz"], 3)}
         out[L] = res
     print(json.dumps(out))
 

@@ -960,11 +960,14 @@ __global__ __launch_bounds__(L4_THREADS) void k_encrypt_long4(EncArgs a) {
     clk.start(a.clk);
     const Lanes LN(threadIdx.x & 31u);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    // RNSTOK_L4_HASH_FIRST: the hashing waves are waves 0-1 (SIMDs 0-1) and
-    // the first tokens' AES wave is wave 2, so a launch of a few tokens runs
-    // its AES and hashing chains on different SIMDs (else waves 0 and 8 shared
-    // SIMD 0); a full workgroup puts the same roles on each SIMD either way.
-    const uint32_t hw = RNSTOK_L4_HASH_FIRST ? (wave < L4_HASH_WAVES ? L4_AES_WAVES + wave : wave - L4_HASH_WAVES) : wave;
+    // RNSTOK_L4_HASH_FIRST: in a launch of at most 64 tokens the hashing
+    // waves are waves 0-1 and the first tokens' AES wave is wave 2, so its
+    // AES and hashing chains run on different SIMDs (else waves 0 and 8 shared
+    // SIMD 0): one 383-B token -2 %.  Full workgroups keep the AES waves
+    // first: hashing first there cost the c4 rank share's encrypt 2.24 ->
+    // 3.39 M cycles (profiles/r06_latency_kernels/c4_share_hash_first.txt).
+    const bool hf = RNSTOK_L4_HASH_FIRST && a.n <= L4_HASH_TOK;                 // launch-uniform
+    const uint32_t hw = hf ? (wave < L4_HASH_WAVES ? L4_AES_WAVES + wave : wave - L4_HASH_WAVES) : wave;
     const bool aes = hw < L4_AES_WAVES;
     const uint32_t col = threadIdx.x & 3u;
     const bool hash_lane = aes || lane < L4_HASH_TOK;
